@@ -1,0 +1,107 @@
+/*
+ * miner_score.h — C ABI of libminer_hip.so, the MI355X (gfx950) scoring path of MINER.
+ *
+ * The reference (MrRobot2211/miner @ 2024-08-07) has no FFI: its boundary is the Python
+ * nn.Module contract of src/model/model.py. These entry points replace the tensor math of that
+ * contract, one per reference interface, and are what a ctypes binding in the reference's
+ * src/model/model.py would call (the binding is shown in INTEGRATION.md):
+ *
+ *   miner_score(..., score_type = WEIGHTED|MAX|MEAN)
+ *       replaces Miner.forward after the news encoder, src/model/model.py:113-138
+ *       (PolyAttention.forward :159-185 -> Cand·muiᵀ :127 -> aggregation :128-136, with
+ *       TargetAwareAttention.forward :200-216 for 'weighted').
+ *   miner_score(..., score_type = NONE)
+ *       replaces PolyAttention.forward alone, src/model/model.py:159-185 (user_out required).
+ *   miner_target_aware(...)
+ *       replaces TargetAwareAttention.forward, src/model/model.py:200-216.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is caller-owned DEVICE memory, row-major and contiguous, 16-byte aligned;
+ *     nothing is allocated inside, nothing synchronises: work is enqueued on `stream`
+ *     (a hipStream_t; NULL = the default stream) and the call returns immediately;
+ *   - `dtype` selects the element type of the activation AND weight tensors
+ *     (MINER_DTYPE_F32 = exact fp32 arithmetic, the parity mode; MINER_DTYPE_BF16 = bf16 operands
+ *     with fp32 accumulation, the throughput mode). Masks are uint8 (0/1, torch.bool storage),
+ *     offsets int32, bias/scores/user_out fp32;
+ *   - return 0 on success, a negative MINER_E* code for invalid arguments (nothing launched), or a
+ *     positive hipError_t from the launch. miner_strerror() names the code.
+ *   - no global state beyond a cached device-attribute query: thread-safe per stream.
+ */
+#ifndef MINER_SCORE_H
+#define MINER_SCORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MINER_ABI_VERSION 1
+
+enum miner_dtype { MINER_DTYPE_F32 = 0, MINER_DTYPE_BF16 = 1 };
+
+/* src/model/model.py:128-136 ('weighted' = TargetAwareAttention). NONE = PolyAttention only. */
+enum miner_score_type {
+  MINER_SCORE_WEIGHTED = 0,
+  MINER_SCORE_MAX = 1,
+  MINER_SCORE_MEAN = 2,
+  MINER_SCORE_NONE = 3
+};
+
+enum miner_error {
+  MINER_OK = 0,
+  MINER_EINVAL = -1,      /* null pointer, bad enum, non-positive size */
+  MINER_ESHAPE = -2,      /* shape outside what this build supports (see miner_supported) */
+  MINER_EALIGN = -3,      /* a pointer is not 16-byte aligned */
+  MINER_ELDS = -4         /* the shape needs more LDS than one CU has */
+};
+
+/*
+ * Score B impressions.
+ *   history      [B, L, d]  dtype  clicked-news embeddings, left-padded (reader.py:369)
+ *   his_mask     [B, L]     uint8  1 = real click, 0 = pad (entities.py:395)
+ *   his_bias     [B, L]     fp32   optional category bias, already averaged over the candidates
+ *                                  (model.py:113-122, :176); NULL = use_category_bias off
+ *   candidates   [sum C_b, d] dtype candidate-news embeddings, impression-major
+ *   cand_offsets [B + 1]    int32  optional CSR offsets of each impression's candidates;
+ *                                  NULL = dense, C_b = C for every impression
+ *   w_poly       [Dc, d]    dtype  poly_attn.linear.weight        (model.py:155)
+ *   context_codes[K, Dc]    dtype  poly_attn.context_codes        (model.py:156-157)
+ *   w_target     [d, d]     dtype  target_aware_attn.linear.weight (model.py:198); may be NULL
+ *                                  unless score_type == WEIGHTED
+ *   scores       [sum C_b]  fp32   matching scores (model.py:138 second output); may be NULL
+ *                                  only when score_type == NONE
+ *   user_out     [B, K, d]  fp32   optional multi_user_interest (model.py:138 first output)
+ */
+int miner_score(void* stream, int dtype, int score_type,
+                const void* history, const uint8_t* his_mask, const float* his_bias,
+                const void* candidates, const int32_t* cand_offsets,
+                const void* w_poly, const void* context_codes, const void* w_target,
+                int B, int L, int C, int d, int Dc, int K,
+                float* scores, float* user_out);
+
+/*
+ * TargetAwareAttention.forward (model.py:200-216) on its own:
+ *   query [B, K, d] dtype (multi_user_interest), key [sum C_b, d] dtype (candidates),
+ *   value [sum C_b, K] fp32 (matching scores Cand·muiᵀ), w_target [d, d] dtype -> out [sum C_b] fp32.
+ */
+int miner_target_aware(void* stream, int dtype,
+                       const void* query, const void* key, const float* value,
+                       const int32_t* cand_offsets, const void* w_target,
+                       int B, int C, int d, int K, float* out);
+
+/* 0 if (dtype, L, d, Dc, K) is supported by this build, else the MINER_E* code miner_score
+ * would return. Host-only, no device call. */
+int miner_supported(int dtype, int L, int d, int Dc, int K);
+
+/* LDS bytes one workgroup of miner_score uses for this shape (host-only). */
+int miner_lds_bytes(int dtype, int score_type, int L, int d);
+
+const char* miner_strerror(int code);
+int miner_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MINER_SCORE_H */

@@ -1,0 +1,63 @@
+"""ctypes binding of libminer_hip.so (declared in include/miner_score.h).
+
+Loading is lazy so that the host-only parts of the package (evaluator, sharding, config parsing)
+import on a machine without the library; every scoring entry point calls ``lib()``, which raises
+loudly when the HIP library is missing — there is no CPU fallback in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MINER_HIP_LIB", os.path.join(_HERE, "libminer_hip.so"))
+
+# enums of include/miner_score.h
+DTYPE_F32, DTYPE_BF16 = 0, 1
+SCORE_WEIGHTED, SCORE_MAX, SCORE_MEAN, SCORE_NONE = 0, 1, 2, 3
+SCORE_TYPES = {"weighted": SCORE_WEIGHTED, "max": SCORE_MAX, "mean": SCORE_MEAN, "none": SCORE_NONE}
+ABI_VERSION = 1
+
+# every symbol include/miner_score.h declares: name -> (restype, argtypes)
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+SIGNATURES = {
+    "miner_score": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "miner_target_aware": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "miner_supported": (_I, [_I, _I, _I, _I, _I]),
+    "miner_lds_bytes": (_I, [_I, _I, _I, _I]),
+    "miner_strerror": (ctypes.c_char_p, [_I]),
+    "miner_abi_version": (_I, []),
+}
+
+_lib = None
+
+
+class MinerLibraryError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library; raises MinerLibraryError if it is missing or ABI-incompatible."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MinerLibraryError(
+            f"{LIB_PATH} not found: build it with `python -m miner_amd.build` "
+            "(the MINER scoring path has no CPU fallback)")
+    handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    if handle.miner_abi_version() != ABI_VERSION:
+        raise MinerLibraryError(f"ABI mismatch: library {handle.miner_abi_version()} != {ABI_VERSION}")
+    _lib = handle
+    return _lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        msg = lib().miner_strerror(code).decode()
+        raise RuntimeError(f"{what} failed with code {code}: {msg}")

@@ -1,0 +1,47 @@
+"""Build libminer_hip.so (the HIP/CDNA4 scoring kernels + C ABI) in-tree for gfx950.
+
+    python -m miner_amd.build            # -> miner_amd/libminer_hip.so
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the build container; the .so then
+travels with the repo snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "miner_score.hip")
+LIB = os.path.join(HERE, "libminer_hip.so")
+ARCH = os.environ.get("MINER_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc"), shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libminer_hip.so)")
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    """Compile csrc/miner_score.hip -> miner_amd/libminer_hip.so (skipped when up to date)."""
+    deps = [SRC, os.path.join(ROOT, "include", "miner_score.h")]
+    if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(p) for p in deps):
+        return LIB
+    tmp = LIB + f".tmp{os.getpid()}"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), SRC, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build_library(force="--force" in sys.argv, verbose=True))

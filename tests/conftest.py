@@ -1,0 +1,38 @@
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+
+
+def golden_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+
+
+def load_golden(name):
+    z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
+    g = {k: z[k] for k in z.files}
+    for k in ("B", "L", "K", "d", "Dc", "C", "use_bias"):
+        g[k] = int(g[k])
+    g["score_type"] = str(g["score_type"])
+    table = g["table"]
+    g["E"] = table[g["his_ids"]]
+    g["cand"] = table[g["cand_ids"]]
+    g["metrics"] = {str(k): float(v) for k, v in zip(g["metric_names"], g["metric_values"])}
+    return g
+
+
+@pytest.fixture(params=golden_names())
+def golden(request):
+    return load_golden(request.param)

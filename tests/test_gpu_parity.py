@@ -1,0 +1,180 @@
+"""HIP kernel parity vs the reference (golden fixtures) and the oracle — needs an MI355X.
+
+Tolerances:
+* fp32 mode (MINER_DTYPE_F32): |x - ref| <= 1e-5*|ref| + 1e-5*rms(ref)   (north_star 1e-5 relative;
+  SURVEY.md §8c absolute floor for near-zero scores).
+* bf16 mode: compared with the oracle evaluated in fp32 on the SAME bf16-rounded inputs and weights;
+  the kernel also rounds its on-chip intermediates (tanh(E·W1ᵀ), attention weights, mui, gelu
+  output) to bf16 MFMA operands, so the bound is |x - ref| <= 2e-2*|ref| + 6e-2*rms(ref), and the
+  AUC computed from bf16 scores must stay within 5e-3 of the fp32 AUC.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import miner_oracle as orc
+from tests.conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _ops():
+    from miner_amd import ops
+    return ops
+
+
+def _dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t if dtype is None else t.to(dtype)
+
+
+def _inputs(g, dtype):
+    W2 = _dev(g["W2"], dtype) if "W2" in g else None
+    bias = _dev(g["bias"], torch.float32) if g["use_bias"] else None
+    return (_dev(g["E"], dtype), _dev(g["his_mask"]), _dev(g["cand"], dtype), _dev(g["W1"], dtype),
+            _dev(g["Q"], dtype), W2, bias)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_fp32_matches_reference(name):
+    g = load_golden(name)
+    E, M, Cd, W1, Q, W2, bias = _inputs(g, torch.float32)
+    scores, mui = _ops().score(E, M, Cd, W1, Q, W2, score_type=g["score_type"], his_bias=bias, return_user=True)
+    torch.cuda.synchronize()
+    ok, worst = orc.parity_ok(scores.cpu().numpy(), g["scores"])
+    assert ok, f"{name}: scores off by {worst:.2f}x the tolerance"
+    ok, worst = orc.parity_ok(mui.cpu().numpy(), g["mui"])
+    assert ok, f"{name}: mui off by {worst:.2f}x the tolerance"
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_poly_attention_alone(name):
+    g = load_golden(name)
+    E, M, _, W1, Q, _, bias = _inputs(g, torch.float32)
+    mui = _ops().poly_attention(E, M, W1, Q, his_bias=bias)
+    torch.cuda.synchronize()
+    ok, worst = orc.parity_ok(mui.cpu().numpy(), g["mui"])
+    assert ok, f"{name}: mui off by {worst:.2f}x the tolerance"
+
+
+@pytest.mark.parametrize("name", [n for n in golden_names() if load_golden(n)["score_type"] == "weighted"])
+def test_target_aware_alone(name):
+    g = load_golden(name)
+    mui = torch.from_numpy(g["mui"])
+    cand = torch.from_numpy(g["cand"])
+    W2 = torch.from_numpy(g["W2"])
+    value = torch.matmul(cand, mui.permute(0, 2, 1))
+    ref = orc.target_aware_torch(mui, cand, value, W2)
+    out = _ops().target_aware(mui.to(DEV), cand.to(DEV), value.to(DEV), W2.to(DEV))
+    torch.cuda.synchronize()
+    ok, worst = orc.parity_ok(out.cpu().numpy(), ref.numpy())
+    assert ok, f"{name}: TAA off by {worst:.2f}x the tolerance"
+
+
+def _bf16_round(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(torch.bfloat16).to(torch.float32)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_bf16_within_tolerance(name):
+    g = load_golden(name)
+    E, M, Cd, W1, Q, W2, bias = _inputs(g, torch.bfloat16)
+    scores = _ops().score(E, M, Cd, W1, Q, W2, score_type=g["score_type"], his_bias=bias)
+    torch.cuda.synchronize()
+    _, ref = orc.score_torch(_bf16_round(g["E"]), torch.from_numpy(g["his_mask"]), _bf16_round(g["cand"]),
+                             _bf16_round(g["W1"]), _bf16_round(g["Q"]),
+                             _bf16_round(g["W2"]) if "W2" in g else None, g["score_type"],
+                             torch.from_numpy(g["bias"]) if g["use_bias"] else None)
+    ok, worst = orc.parity_ok(scores.cpu().numpy(), ref.numpy(), rtol=2e-2, rms_floor=6e-2)
+    assert ok, f"{name}: bf16 scores off by {worst:.2f}x the bf16 tolerance"
+
+
+def test_ragged_equals_dense():
+    g = load_golden("cfg3_slice")
+    E, M, Cd, W1, Q, W2, _ = _inputs(g, torch.float32)
+    dense = _ops().score(E, M, Cd, W1, Q, W2)
+    B, C, d = Cd.shape
+    # drop a different number of trailing candidates per impression -> ragged CSR batch
+    keep = [C - 3 * b for b in range(B)]
+    packed = torch.cat([Cd[b, :keep[b]] for b in range(B)])
+    offs = torch.tensor([0] + list(np.cumsum(keep)), dtype=torch.int32, device=DEV)
+    rag = _ops().score(E, M, packed, W1, Q, W2, cand_offsets=offs)
+    torch.cuda.synchronize()
+    want = torch.cat([dense[b, :keep[b]] for b in range(B)])
+    ok, worst = orc.parity_ok(rag.cpu().numpy(), want.cpu().numpy())
+    assert ok, worst
+
+
+def test_many_candidates_chunked():
+    """C > 64 exercises the multi-chunk S6/S7 loop; compared with the fp64 oracle."""
+    rng = np.random.default_rng(11)
+    B, L, K, d, Dc, C = 3, 30, 32, 128, 64, 150
+    E = (rng.standard_normal((B, L, d)) / np.sqrt(d)).astype(np.float32)
+    cand = (rng.standard_normal((B, C, d)) / np.sqrt(d)).astype(np.float32)
+    mask = rng.random((B, L)) < 0.7
+    W1 = ((rng.random((Dc, d)) * 2 - 1) / np.sqrt(d)).astype(np.float32)
+    Q = ((rng.random((K, Dc)) * 2 - 1) * 0.2).astype(np.float32)
+    W2 = ((rng.random((d, d)) * 2 - 1) / np.sqrt(d)).astype(np.float32)
+    s = _ops().score(_dev(E), _dev(mask), _dev(cand), _dev(W1), _dev(Q), _dev(W2))
+    torch.cuda.synchronize()
+    _, ref = orc.score_f64(E, mask, cand, W1, Q, W2)
+    ok, worst = orc.parity_ok(s.cpu().numpy(), ref)
+    assert ok, worst
+
+
+def test_config3_batch_properties():
+    """Full config-3 shapes (L=50, K=32, d=768, Dc=200, C=40), several thousand impressions:
+    a strided sample is checked against the oracle, and every impression's score is independent
+    of the batch it is scored in (a shuffled sub-batch reproduces it)."""
+    from miner_amd import synthetic
+    B = 4096
+    imp = synthetic.impressions(36, 0, B, L=50, d=768, C=40, device=DEV)
+    W1, Q, W2 = synthetic.init_weights(36, 768, 200, 32, device=DEV)
+    s = _ops().score(imp.history, imp.his_mask, imp.candidates, W1, Q, W2)
+    idx = torch.arange(0, B, 97, device=DEV)
+    _, ref = orc.score_torch(imp.history[idx].cpu(), imp.his_mask[idx].cpu(), imp.candidates[idx].cpu(),
+                             W1.cpu(), Q.cpu(), W2.cpu())
+    ok, worst = orc.parity_ok(s[idx].cpu().numpy(), ref.numpy())
+    assert ok, worst
+    perm = torch.randperm(B, device=DEV)[:1000]
+    s2 = _ops().score(imp.history[perm], imp.his_mask[perm], imp.candidates[perm], W1, Q, W2)
+    ok, worst = orc.parity_ok(s2.cpu().numpy(), s[perm].cpu().numpy(), rtol=1e-6, rms_floor=1e-6)
+    assert ok, worst
+    assert torch.isfinite(s).all()
+
+
+def test_bf16_config3_auc_delta():
+    from miner_amd import synthetic
+    from miner_amd.evaluation import auc_score
+    B = 2048
+    imp = synthetic.impressions(36, 0, B, L=50, d=768, C=40, device=DEV)
+    W1, Q, W2 = synthetic.init_weights(36, 768, 200, 32, device=DEV)
+    s32 = _ops().score(imp.history, imp.his_mask, imp.candidates, W1, Q, W2)
+    bf = torch.bfloat16
+    s16 = _ops().score(imp.history.to(bf), imp.his_mask, imp.candidates.to(bf), W1.to(bf), Q.to(bf), W2.to(bf))
+    lab = imp.labels.reshape(-1).cpu().numpy()
+    a32 = auc_score(lab, torch.sigmoid(s32).reshape(-1).cpu().numpy())
+    a16 = auc_score(lab, torch.sigmoid(s16).reshape(-1).cpu().numpy())
+    assert abs(a32 - a16) < 5e-3, (a32, a16)
+
+
+def test_unsupported_shape_raises():
+    E = torch.zeros((2, 4, 64), device=DEV)
+    M = torch.ones((2, 4), dtype=torch.bool, device=DEV)
+    C = torch.zeros((2, 3, 64), device=DEV)
+    W1 = torch.zeros((8, 64), device=DEV)
+    Q = torch.zeros((65, 8), device=DEV)   # K = 65 > 32 in this build
+    W2 = torch.zeros((64, 64), device=DEV)
+    with pytest.raises(ValueError):
+        _ops().score(E, M, C, W1, Q, W2)
+    with pytest.raises(ValueError):
+        _ops().score(E, M, C, W1, Q[:4], W2, score_type="bogus")
+
+
+def test_cpu_tensors_fail_loudly():
+    E = torch.zeros((2, 4, 64))
+    with pytest.raises(RuntimeError):
+        _ops().score(E, torch.ones((2, 4), dtype=torch.bool), torch.zeros((2, 3, 64)),
+                     torch.zeros((8, 64)), torch.zeros((4, 8)), torch.zeros((64, 64)))
