@@ -1,0 +1,225 @@
+"""Benchmark: scored (user, candidate) pairs/s of the fused MINER scoring kernel on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]            # N=1 default
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json metric, config 3 "MIND-large shape"): history L=50, K=32 interests,
+d=768, Dc=200, C=40 candidates per impression, bf16 operands / fp32 accumulation, synthetic
+impressions already resident in HBM. One step = one launch of the fused kernel over a batch of
+``--batch`` impressions per GPU; impressions are sharded across ranks with no collective on the
+data path (weak scaling); ``value`` = pairs scored by all ranks / max-over-ranks time.
+
+Also reported (same JSON line): the roofline of the dominant kernel (algorithmic FLOPs / bytes per
+launch over the HIP-event launch time, on the stream the kernel is launched on), the fp32 parity
+mode's throughput, and the CPU baseline (the oracle — a restatement of the reference's torch CPU
+path — timed on this host's cores over a bounded sample) on rank 0 at N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+L, K, D, DC, C = 50, 32, 768, 200, 40
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3        # fp32 MFMA / vector
+PEAK_HBM_GBS = 8000.0          # HBM3E spec
+
+
+def flops_per_impression(L, K, d, Dc, C):
+    """Algorithmic FLOPs: 2LdDc + 2LDcK + 2KLd + 2Kd² + 4CdK + 2CK."""
+    return 2 * L * d * Dc + 2 * L * Dc * K + 2 * K * L * d + 2 * K * d * d + 4 * C * d * K + 2 * C * K
+
+
+def bytes_per_impression(L, d, C, elem):
+    """Algorithmic HBM bytes: (L + C)·d·s + L (mask) + 4C (fp32 scores); weights excluded."""
+    return (L + C) * d * elem + L + 4 * C
+
+
+def cpu_baseline(seconds: float = 15.0):
+    """Oracle (torch fp32 CPU restatement of model.py:159-216,127) on host cores."""
+    from miner_amd import synthetic
+    from oracle import miner_oracle as orc
+    threads = torch.get_num_threads()
+    imp = synthetic.impressions(36, 0, 512, L=L, d=D, C=C, device="cpu")
+    W1, Q, W2 = synthetic.init_weights(36, D, DC, K)
+    bs = 64
+    # batched layout: 64 impressions x 40 candidates per call
+    with torch.no_grad():
+        orc.score_torch(imp.history[:bs], imp.his_mask[:bs], imp.candidates[:bs], W1, Q, W2)  # warmup
+        pairs, t0, i = 0, time.perf_counter(), 0
+        while True:
+            lo = (i * bs) % 512
+            orc.score_torch(imp.history[lo:lo + bs], imp.his_mask[lo:lo + bs], imp.candidates[lo:lo + bs], W1, Q, W2)
+            pairs += bs * C
+            i += 1
+            el = time.perf_counter() - t0
+            if el > seconds and i >= 2:
+                break
+        batched = pairs / el
+        # reference-faithful layout: one candidate per sample, eval_batch_size 32
+        n_imp = 0
+        t0 = time.perf_counter()
+        while True:
+            lo = n_imp % 512
+            orc.score_per_candidate_torch(imp.history[lo:lo + 2], imp.his_mask[lo:lo + 2],
+                                          imp.candidates[lo:lo + 2], W1, Q, W2, batch_size=32)
+            n_imp += 2
+            el2 = time.perf_counter() - t0
+            if el2 > seconds / 3 and n_imp >= 2:
+                break
+        per_cand = n_imp * C / el2
+    return {"value": round(batched, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{pairs // C} impressions x {C} candidates (L={L},K={K},d={D},Dc={DC}), fp32, "
+                      f"batched 64 impressions/call, {el:.1f}s",
+            "per_candidate_value": round(per_cand, 1),
+            "per_candidate_sample": f"{n_imp} impressions, one candidate per sample, batch 32 "
+                                    f"(reader.py:376-379 layout), {el2:.1f}s"}
+
+
+def load_traffic(path):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == f"L{L}_K{K}_d{D}_Dc{DC}_C{C}_bf16":
+            return t
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32768, help="impressions per GPU per step")
+    ap.add_argument("--pool", type=int, default=2, help="distinct resident batches per GPU")
+    ap.add_argument("--fp32-steps", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from miner_amd import ops, synthetic
+
+    B = args.batch
+    bf = torch.bfloat16
+    pool = []
+    for p in range(args.pool):
+        start = (rank * args.pool + p) * B      # each rank scores its own shard
+        imp = synthetic.impressions(36, start, B, L=L, d=D, C=C, device=dev, dtype=bf)
+        pool.append(imp)
+    W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
+    pw16 = ops.pack_weights(W1, Q, W2, dtype=bf)        # once per model, outside the timed region
+    pw32 = ops.pack_weights(W1, Q, W2, dtype=torch.float32)
+    out = torch.empty((B, C), device=dev, dtype=torch.float32)
+    torch.cuda.synchronize()
+
+    def step(i):
+        imp = pool[i % len(pool)]
+        return ops.score(imp.history, imp.his_mask, imp.candidates, pw16)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        out = step(i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out).all()
+
+    # fp32 parity mode on the same impressions (fewer steps: it runs at the fp32 MFMA rate)
+    f32 = None
+    if args.fp32_steps > 0:
+        imp = pool[0]
+        h32, c32 = imp.history.float(), imp.candidates.float()
+        ops.score(h32, imp.his_mask, c32, pw32)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(args.fp32_steps):
+            ops.score(h32, imp.his_mask, c32, pw32)
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms32 = a.elapsed_time(b) / args.fp32_steps
+        f32 = {"value": round(B * C / (ms32 / 1e3), 1), "unit": "pairs/s", "ms_per_step": round(ms32, 3),
+               "tflops": round(flops_per_impression(L, K, D, DC, C) * B / (ms32 / 1e3) / 1e12, 2),
+               "frac_fp32_peak": round(flops_per_impression(L, K, D, DC, C) * B / (ms32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)}
+        del h32, c32
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    pairs_total = B * C * args.steps * world
+    value = pairs_total / elapsed
+    fl = flops_per_impression(L, K, D, DC, C) * B
+    by = bytes_per_impression(L, D, C, 2) * B
+    tflops = fl / (kern_ms / 1e3) / 1e12
+    gbs = by / (kern_ms / 1e3) / 1e9
+    traffic = load_traffic(args.traffic)
+    traffic_bytes = None
+    if traffic and traffic.get("batch") == B:
+        traffic_bytes = traffic.get("hbm_bytes_per_launch")
+    roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic_bytes,
+            "kernel": "miner_fused<bf16,full>", "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4)}
+    roof_hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_launch": by,
+                "traffic": traffic_bytes}
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_seconds)
+    line = {
+        "metric": "(user,candidate) scores/sec at history=50,K=32,d=768; AUC parity vs ref",
+        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (seeded MIND-large-shaped impressions, random-init weights)",
+        "config": {"workload": "config 3 MIND-large shape", "history": L, "K": K, "d": D, "Dc": DC,
+                   "candidates": C, "impressions_per_gpu_per_step": B, "global_batch": B * world,
+                   "parallelism": f"dp{world} (impression shards, no data-path collective)"},
+        "roofline": roof, "roofline_hbm": roof_hbm, "fp32_parity_mode": f32, "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -6,6 +6,9 @@
  * contract, one per reference interface, and are what a ctypes binding in the reference's
  * src/model/model.py would call (the binding is shown in INTEGRATION.md):
  *
+ *   miner_pack_weights(...)
+ *       one-time repack of the module parameters poly_attn.linear.weight, poly_attn.context_codes
+ *       and target_aware_attn.linear.weight (model.py:155-157, :198) into the kernel layout.
  *   miner_score(..., score_type = WEIGHTED|MAX|MEAN)
  *       replaces Miner.forward after the news encoder, src/model/model.py:113-138
  *       (PolyAttention.forward :159-185 -> Cand·muiᵀ :127 -> aggregation :128-136, with
@@ -30,13 +33,14 @@
 #ifndef MINER_SCORE_H
 #define MINER_SCORE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define MINER_ABI_VERSION 1
+#define MINER_ABI_VERSION 2
 
 enum miner_dtype { MINER_DTYPE_F32 = 0, MINER_DTYPE_BF16 = 1 };
 
@@ -57,6 +61,20 @@ enum miner_error {
 };
 
 /*
+ * Weights, packed once per model (they are static during evaluation) into the kernel's tiled
+ * layout: 32-row x 32-column tiles, rows in the order the MFMA accumulators want them, zero padded
+ * (see DESIGN.md "Packed weights").  `packed` is caller-owned device memory of
+ * miner_packed_weights_bytes() bytes, 16-byte aligned.
+ *   w_poly        [Dc, d]  dtype  poly_attn.linear.weight          (model.py:155)
+ *   context_codes [K, Dc]  dtype  poly_attn.context_codes          (model.py:156-157)
+ *   w_target      [d, d]   dtype  target_aware_attn.linear.weight  (model.py:198); NULL when the
+ *                                 model has no TargetAwareAttention (score_type max/mean)
+ */
+size_t miner_packed_weights_bytes(int dtype, int d, int Dc, int K);
+int miner_pack_weights(void* stream, int dtype, const void* w_poly, const void* context_codes,
+                       const void* w_target, int d, int Dc, int K, void* packed);
+
+/*
  * Score B impressions.
  *   history      [B, L, d]  dtype  clicked-news embeddings, left-padded (reader.py:369)
  *   his_mask     [B, L]     uint8  1 = real click, 0 = pad (entities.py:395)
@@ -65,29 +83,27 @@ enum miner_error {
  *   candidates   [sum C_b, d] dtype candidate-news embeddings, impression-major
  *   cand_offsets [B + 1]    int32  optional CSR offsets of each impression's candidates;
  *                                  NULL = dense, C_b = C for every impression
- *   w_poly       [Dc, d]    dtype  poly_attn.linear.weight        (model.py:155)
- *   context_codes[K, Dc]    dtype  poly_attn.context_codes        (model.py:156-157)
- *   w_target     [d, d]     dtype  target_aware_attn.linear.weight (model.py:198); may be NULL
- *                                  unless score_type == WEIGHTED
+ *   packed_weights          dtype  miner_pack_weights() output (w_target packed when
+ *                                  score_type == WEIGHTED)
  *   scores       [sum C_b]  fp32   matching scores (model.py:138 second output); may be NULL
  *                                  only when score_type == NONE
  *   user_out     [B, K, d]  fp32   optional multi_user_interest (model.py:138 first output)
  */
 int miner_score(void* stream, int dtype, int score_type,
                 const void* history, const uint8_t* his_mask, const float* his_bias,
-                const void* candidates, const int32_t* cand_offsets,
-                const void* w_poly, const void* context_codes, const void* w_target,
+                const void* candidates, const int32_t* cand_offsets, const void* packed_weights,
                 int B, int L, int C, int d, int Dc, int K,
                 float* scores, float* user_out);
 
 /*
  * TargetAwareAttention.forward (model.py:200-216) on its own:
  *   query [B, K, d] dtype (multi_user_interest), key [sum C_b, d] dtype (candidates),
- *   value [sum C_b, K] fp32 (matching scores Cand·muiᵀ), w_target [d, d] dtype -> out [sum C_b] fp32.
+ *   value [sum C_b, K] fp32 (matching scores Cand·muiᵀ), packed_weights with w_target packed
+ *   (Dc = the context-code dim they were packed with) -> out [sum C_b] fp32.
  */
 int miner_target_aware(void* stream, int dtype,
                        const void* query, const void* key, const float* value,
-                       const int32_t* cand_offsets, const void* w_target,
+                       const int32_t* cand_offsets, const void* packed_weights, int Dc,
                        int B, int C, int d, int K, float* out);
 
 /* 0 if (dtype, L, d, Dc, K) is supported by this build, else the MINER_E* code miner_score
@@ -95,7 +111,7 @@ int miner_target_aware(void* stream, int dtype,
 int miner_supported(int dtype, int L, int d, int Dc, int K);
 
 /* LDS bytes one workgroup of miner_score uses for this shape (host-only). */
-int miner_lds_bytes(int dtype, int score_type, int L, int d);
+int miner_lds_bytes(int dtype, int score_type, int L, int d, int Dc);
 
 const char* miner_strerror(int code);
 int miner_abi_version(void);

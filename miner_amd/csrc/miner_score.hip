@@ -1,28 +1,43 @@
 // miner_score.hip — fused MINER scoring kernel for MI355X (gfx950 / CDNA4).
 //
-// One workgroup (8 waves, 512 threads) scores one impression at a time and walks impressions
-// b = blockIdx.x, blockIdx.x + gridDim.x, ...  Everything between the HBM reads of the
-// impression's history/candidate rows and the fp32 score writes stays on chip:
+// One workgroup (8 waves, 512 threads, one per CU) scores one impression at a time and walks
+// impressions b = blockIdx.x, blockIdx.x + gridDim.x, ...  Everything between the HBM reads of an
+// impression's history/candidate rows and its fp32 score writes stays on chip:
 //
-//   S0  history rows E[L,d] -> LDS (bf16 mode; fp32 mode streams them from L2 instead)
-//   S1  Pᵀ = tanh(W1 · Eᵀ)          [Dc,L]   MFMA, wave w owns Dc-tile w          (model.py:171)
-//   S2  Sᵀ = Q · Pᵀ                 [K,L]    MFMA on the S1 accumulators, ds_add  (model.py:174)
-//   S3  A  = softmax_L(fill(Sᵀ))   [K,L]    wave shuffles; masked -> 1e-30       (model.py:178-181)
-//   S4  mui = A · E                 [K,d]    MFMA (E read transposed from LDS)    (model.py:182)
-//   S5  X  = gelu(W2 · muiᵀ)       [d,K]    MFMA, wave w owns d-tiles w, w+8, .. (model.py:212)
-//   S6  Lgᵀ = Xᵀ·Candᵀ, Mᵀ = mui·Candᵀ [K,C] MFMA on the S5 accumulators, ds_add (model.py:127,213)
-//   S7  score_c = Σ_k softmax_K(Lg)_k · M_k  (or max_k / mean_k of M)            (model.py:128-134,213-214)
+//   S0  history rows E[L,d] -> LDS by LDS-DMA (bf16; the fp32 parity mode reads them from L2)
+//   S1  Pᵀ = tanh(W1 · Eᵀ)        [Dc,L]  MFMA, wave w owns Dc-tile w; P -> LDS   (model.py:171)
+//   S2  Sᵀ = Q · Pᵀ               [K,L]   MFMA, one wave per 32-position tile      (model.py:174)
+//   S3  A  = softmax_L(fill(Sᵀ))  [K,L]   wave shuffles; masked -> 1e-30           (model.py:178-181)
+//   S4  mui = A · E               [K,d]   MFMA, Eᵀ read with ds_read_b64_tr_b16    (model.py:182)
+//   S5  X  = gelu(W2 · muiᵀ)      [d,K]   MFMA, wave w owns d-tiles w, w+8, w+16   (model.py:212)
+//   S6  Lgᵀ = Xᵀ·Candᵀ, Mᵀ = mui·Candᵀ  [K,C]  MFMA split over the waves' d-tiles,
+//       reduced through LDS with plain stores in two rounds                     (model.py:127,213)
+//   S7  score_c = Σ_k softmax_K(Lg)_k · M_k  (or max_k / mean_k of M)      (model.py:128-134,213-214)
 //
-// Operand layout (both dtypes) — "slab" = 32 consecutive contraction indices:
-//   lane l = 32h + r (h = l>>5, r = l&31) holds 16 contiguous elements [16h, 16h+16) of row r of
-//   the slab.  bf16: two v_mfma_f32_32x32x16_bf16 steps (8 elements each); fp32: sixteen
-//   v_mfma_f32_32x32x2_f32 steps (1 element each, exact fp32 fma chain).  The accumulator of a
-//   32x32 MFMA tile keeps row (e&3)+8(e>>2)+4h of column r in register e; loading the A-operand
-//   rows of a GEMM in the order pi(r) = 16((r>>2)&1) + (r&3) + 4(r>>3) makes register e of lane
-//   half h hold row 16h+e — i.e. the accumulator IS a slab fragment of the next contraction, with
-//   no LDS round trip (S1->S2, S5->S6).
+// Operand layout (both dtypes) — a "slab" is 32 consecutive contraction indices: lane
+// l = 32h + r (h = l>>5, r = l&31) holds 16 contiguous elements [16h, 16h+16) of row r of the
+// slab. bf16: two v_mfma_f32_32x32x16_bf16 steps (8 elements each); fp32: sixteen
+// v_mfma_f32_32x32x2_f32 steps (one element each, an exact fp32 fma chain). A 32x32 MFMA
+// accumulator keeps row (e&3)+8(e>>2)+4h of column r in register e; when the A-operand rows of a
+// GEMM are taken in the order pi(r) = 16((r>>2)&1) + (r&3) + 4(r>>3), register e of lane half h
+// holds row 16h+e: the accumulator IS a slab fragment of a following contraction over its rows
+// (S5 -> S6), and its 16 registers are 16 contiguous elements of an LDS row (S1 -> P).
+//
+// Weights are pre-packed once (miner_pack_weights) into 32-row x 32-column tiles, rows in pi
+// order, so each wave-instruction of a weight slab reads 2 KiB (bf16) contiguous bytes: reading
+// the row-major [Dc,d] / [d,d] matrices directly put every wave's 32 row segments on 4 of an XCD
+// L2's 16 channels (row stride 1536 B) and ran S5 3x slower.
+//
+// Hot-loop rules learned on this kernel (ROCm 7.2 hipcc):
+//   * no LDS float atomics on the bf16 path: ds_add_f32 cost ~180 cycles each and serialise;
+//   * every global load in a slab loop is unconditional (addresses clamped): a predicated load
+//     makes hipcc wait vmcnt(0) and drains the prefetch ring; a loop back-edge does the same, so
+//     the slab loops are fully unrolled on a compile-time d (NS = d/32 template);
+//   * lane ids are re-derived from an opaque threadIdx.x in every stage so no per-lane address
+//     is hoisted across stages (the hoisted values were spilled; scratch reloads wait vmcnt(0)).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <math.h>
 
 #include "../../include/miner_score.h"
@@ -33,37 +48,55 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kMaxL = 64;        // history positions per impression (two 32-row tiles)
 constexpr int kMaxK = 32;        // interest vectors (one 32-row tile)
 constexpr int kMaxDc = 256;      // context-code dim (one 32-row tile per wave)
-constexpr int kMaxD = 768;       // embedding dim (<= 3 d-tiles per wave in S5)
+constexpr int kMaxD = 768;       // embedding dim (<= 3 d-tiles per wave)
 constexpr int kMaxJ = kMaxD / 32 / kWaves;
-constexpr int kCChunk = 64;      // candidates per S6/S7 pass
+constexpr int kCChunk = 64;      // candidates per S6/S7 pass (two 32-column tiles)
 constexpr int kLdsMax = 160 * 1024;
+constexpr int kLgS = kCChunk + 1;      // fp32-path Lg/Mt row stride (floats)
+constexpr int kPartS = 36;             // bf16-path partial slab row stride (floats): [c][k] rows
+constexpr int kPartTile = 32 * kPartS; // one 32x32 tile, floats
+constexpr int kPartWave = 4 * kPartTile;  // Lg ct0, Lg ct1, Mt ct0, Mt ct1
 
 enum Mode { kFull = 0, kTaa = 1 };
 
 struct Params {
-  const void* hist;
+  const void* hist;      // kFull: history [B,L,d]; kTaa: query (mui) [B,K,d]
   const uint8_t* mask;
   const float* bias;
   const void* cand;
   const int32_t* cand_off;
-  const void* W1;
-  const void* Q;
-  const void* W2;
-  const float* value;  // TAA mode: [sum C_b, K]
+  const void* wp;        // packed weights (miner_pack_weights)
+  const float* value;    // kTaa: [sum C_b, K]
   float* scores;
   float* mui_out;
   int B, L, C, d, Dc, K, score_type;
   // LDS carve (bytes)
-  int ES;      // history row stride (bf16 mode)
-  int MS;      // mui row stride
-  int offE, offZ, offLg, offMt, offMui, offS, offAw;
+  int MS;       // mui row stride
+  int PS;       // P row stride (elements)
+  int offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt;
+  int dbg;      // ablation bits, honoured only by the -DMINER_STAMPS diagnostic build
 };
+
+// ---------------------------------------------------------------------------------------------
+// packed weight layout (elements of T):  [W1p | Qp | W2p]
+//   W1p: ceil(Dc/32) x (d/32) tiles of 32x32, tile (ct, j) row r = W1[32ct + pi(r)][32j .. 32j+31]
+//   Qp : 32 x 32*ceil(Dc/32), zero padded
+//   W2p: (d/32) x (d/32) tiles, tile (jt, j) row r = W2[32jt + pi(r)][32j .. 32j+31]
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ inline int n_ctiles(int Dc) { return (Dc + 31) >> 5; }
+__host__ __device__ inline size_t w1p_elems(int d, int Dc) { return (size_t)n_ctiles(Dc) * (d >> 5) * 1024; }
+__host__ __device__ inline size_t qp_elems(int Dc) { return (size_t)n_ctiles(Dc) * 1024; }
+__host__ __device__ inline size_t w2p_elems(int d) { return (size_t)(d >> 5) * (d >> 5) * 1024; }
+__host__ __device__ inline int pi_row(int r) { return 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3); }
 
 // ---------------------------------------------------------------------------------------------
 // element helpers
@@ -71,48 +104,37 @@ struct Params {
 template <class T> struct Frag;            // one lane's 16-element slab fragment
 template <> struct Frag<__bf16> { u32x4 q[2]; };
 template <> struct Frag<float> { u32x4 q[4]; };
+template <class T> constexpr int kNQ = sizeof(T);   // u32x4 per fragment (bf16: 2, fp32: 4)
 
 template <class T>
 __device__ __forceinline__ void frag_zero(Frag<T>& f) {
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(f.q) / sizeof(u32x4)); ++i) f.q[i] = u32x4{0u, 0u, 0u, 0u};
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = u32x4{0u, 0u, 0u, 0u};
 }
 
-// 16 contiguous elements from a 16-byte-aligned address (global or LDS).
+// 16 contiguous elements from a 16-byte-aligned address (global or LDS)
 template <class T>
 __device__ __forceinline__ void frag_load(Frag<T>& f, const T* p) {
   const u32x4* s = reinterpret_cast<const u32x4*>(p);
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(f.q) / sizeof(u32x4)); ++i) f.q[i] = s[i];
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = s[i];
 }
 
-__device__ __forceinline__ float to_f32(float x) { return x; }
-__device__ __forceinline__ float to_f32(__bf16 x) { return (float)x; }
+template <class T>
+__device__ __forceinline__ void frag_store(T* p, const Frag<T>& f) {
+  u32x4* s = reinterpret_cast<u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) s[i] = f.q[i];
+}
+
 template <class T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
   __bf16 a = (__bf16)lo, b = (__bf16)hi;
-  unsigned short ua = __builtin_bit_cast(unsigned short, a);
-  unsigned short ub = __builtin_bit_cast(unsigned short, b);
-  return (unsigned)ua | ((unsigned)ub << 16);
+  return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
 }
 
-// 16 elements with a per-element bound (unaligned / ragged rows, e.g. context codes).
-template <class T>
-__device__ __forceinline__ void frag_load_pred(Frag<T>& f, const T* row, int start, int limit) {
-  float v[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) v[e] = (start + e < limit) ? to_f32(row[start + e]) : 0.f;
-  if constexpr (sizeof(T) == 2) {
-#pragma unroll
-    for (int m = 0; m < 8; ++m) f.q[m >> 2][m & 3] = pack_bf16x2(v[2 * m], v[2 * m + 1]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) f.q[e >> 2][e & 3] = __float_as_uint(v[e]);
-  }
-}
-
-// accumulator tile (rows permuted by pi at load time) -> slab fragment of the next contraction
+// accumulator tile (rows taken in pi order) -> 16 contiguous elements / slab fragment
 template <class T>
 __device__ __forceinline__ void acc_to_frag(Frag<T>& f, const f32x16& x) {
   if constexpr (sizeof(T) == 2) {
@@ -140,18 +162,13 @@ __device__ __forceinline__ void mma_slab(f32x16& acc, const Frag<T>& a, const Fr
   }
 }
 
-__device__ __forceinline__ int pi_row(int r) { return 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3); }
 __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
 
-__device__ __forceinline__ float wave_max(float v) {
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  for (int e = 0; e < 16; ++e) z[e] = 0.f;
+  return z;
 }
 
 // torch.nn.functional.gelu(approximate='none')
@@ -162,8 +179,7 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 // operand rounding of that mode.  The fp32 parity mode uses the libm tanhf / erff / expf.
 __device__ __forceinline__ float tanh_fast(float x) {
   const float e = __builtin_amdgcn_exp2f(fminf(2.8853900817779268f * fabsf(x), 126.f));  // e^{2|x|}
-  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
-  return copysignf(t, x);
+  return copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
 }
 __device__ __forceinline__ float gelu_fast(float x) {
   const float z = fabsf(x) * 0.70710678118654752440f;
@@ -178,142 +194,365 @@ template <class T> __device__ __forceinline__ float act_tanh(float x) {
 template <class T> __device__ __forceinline__ float act_gelu(float x) {
   if constexpr (sizeof(T) == 2) return gelu_fast(x); else return gelu_erf(x);
 }
+template <class T> __device__ __forceinline__ float act_exp(float x) {
+  if constexpr (sizeof(T) == 2) return __expf(x); else return expf(x);
+}
 
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
+// ---------------------------------------------------------------------------------------------
+// history image in LDS (bf16 mode)
+// ---------------------------------------------------------------------------------------------
+// Rows of 2d bytes packed back to back — the LDS-DMA (global_load_lds_dwordx4) writes each
+// wave's 1 KiB linearly — with 16-byte chunk c of row `row` stored at chunk c ^ eswz(row).  The
+// XOR is applied on the DMA's per-lane SOURCE address and again on every read: the 16 rows of a
+// ds_read_b128 lane group land in 16 different 16-byte slots (S1) and the 4 rows of a
+// ds_read_b64_tr_b16 block in 4 different 64-byte groups (S4), both conflict-free.
+__device__ __forceinline__ int eswz(int row, int g16) {
+  return g16 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 1) << 2) | ((row >> 1) & 3));
+}
+
+template <class T>
+__device__ __forceinline__ void dma_history(const T* E, int L, int d, char* ldsE, int wave, int lane) {
+  const int cpr = d >> 3;                 // 16-byte chunks per row
+  const int g16 = (cpr & 15) == 0;
+  const int total = L * cpr;
+  const int nblk = (total + 63) >> 6;
+  for (int blk = wave; blk < nblk; blk += kWaves) {
+    const int pos = blk * 64 + lane;
+    const int row = pos / cpr;
+    const int c = pos - row * cpr;
+    const T* src = (pos < total) ? E + (size_t)row * d + (size_t)((c ^ eswz(row, g16)) << 3) : E;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(ldsE + blk * 1024), 16, 0, 0);
+  }
+}
+
+// B-operand slab fragment of history row `row` (contraction over d), from the swizzled image
+__device__ __forceinline__ void frag_load_E(Frag<__bf16>& f, const char* ldsE, int row, int kb, int h, int rowB, int g16) {
+  const int c0 = (kb + 16 * h) >> 3;
+  const int sw = eswz(row, g16);
+  const char* base = ldsE + row * rowB;
+  f.q[0] = *reinterpret_cast<const u32x4*>(base + ((c0 ^ sw) << 4));
+  f.q[1] = *reinterpret_cast<const u32x4*>(base + (((c0 + 1) ^ sw) << 4));
+}
+
+// ---------------------------------------------------------------------------------------------
+// diagnostic stamps (-DMINER_STAMPS only)
+// ---------------------------------------------------------------------------------------------
+#ifdef MINER_STAMPS
+// thread 0 of every workgroup sums the s_memtime cycles each stage takes (between the barriers
+// that delimit it) into g_stage_cycles; p.dbg enables ablations.  Never in the product library.
+__device__ unsigned long long g_stage_cycles[16];
+__device__ unsigned long long g_stage_imps;
+#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } } while (0)
+#define STAMP_FLUSH(n) do { if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stage_cycles[i_], st_acc[i_]); atomicAdd(&g_stage_imps, (unsigned long long)(n)); } } while (0)
+#define DBG(bit) (p.dbg & (1 << (bit)))
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH(n) do {} while (0)
+#define DBG(bit) 0
+#endif
+
+// Lane ids re-derived from an opaque copy of threadIdx.x at the top of every stage (see header).
+#define FRESH_LANE_IDS()                                              \
+  int tid_o_ = threadIdx.x;                                           \
+  asm volatile("" : "+v"(tid_o_));                                    \
+  const int tid = tid_o_;                                             \
+  const int lane = tid & 63;                                          \
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);          \
+  const int r = lane & 31;                                            \
+  const int h = lane >> 5;                                            \
+  (void)tid; (void)lane; (void)wave; (void)r; (void)h
+
+// ---------------------------------------------------------------------------------------------
+// S5 body, specialised on NM = number of d-tiles the wave owns (tiles wave + 8m)
+// ---------------------------------------------------------------------------------------------
+// X_m = gelu(W2[tile m] · muiᵀ) over the whole contraction d; packed W2 slabs stream from L2
+// through a PF-deep register ring (unconditional loads, clamped at the end), muiᵀ fragments come
+// from LDS.  The result stays in registers as slab fragments of the S6 contraction.
+template <class T, int PF, int NM>
+__device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restrict__ W2p, const T* muiL,
+                                        int msE, int d, int wave, int r, int h) {
+  const int ns = d >> 5;
+  f32x16 acc[NM];
+  const T* w2t[NM];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) z[e] = 0.f;
-  return z;
+  for (int m = 0; m < NM; ++m) {
+    acc[m] = zero16();
+    w2t[m] = W2p + (size_t)(wave + kWaves * m) * ns * 1024 + r * 32 + 16 * h;   // tile row r, slab 0
+  }
+  Frag<T> ring[PF][NM];
+#pragma unroll
+  for (int s = 0; s < PF; ++s)
+#pragma unroll
+    for (int m = 0; m < NM; ++m) frag_load(ring[s][m], w2t[m] + min(s, ns - 1) * 1024);
+  int j = 0;
+#pragma unroll
+  for (; j + PF <= ns; j += PF) {
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      Frag<T> bm;
+      frag_load(bm, muiL + r * msE + (j + s) * 32 + 16 * h);
+#pragma unroll
+      for (int m = 0; m < NM; ++m) mma_slab<T>(acc[m], ring[s][m], bm);
+#pragma unroll
+      for (int m = 0; m < NM; ++m) frag_load(ring[s][m], w2t[m] + min(j + s + PF, ns - 1) * 1024);
+      __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < PF; ++s) {
+    if (j + s < ns) {
+      Frag<T> bm;
+      frag_load(bm, muiL + r * msE + (j + s) * 32 + 16 * h);
+#pragma unroll
+      for (int m = 0; m < NM; ++m) mma_slab<T>(acc[m], ring[s][m], bm);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[m][e] = act_gelu<T>(acc[m][e]);
+    acc_to_frag(xf[m], acc[m]);
+  }
+}
+
+// S6 partial products over the wave's d-tiles for candidates [cc, cc+64): lg = Xᵀ·Candᵀ and
+// mt = mui·Candᵀ restricted to those tiles.  Candidate rows past the end are clamped to a real
+// row (finite data, never read back by S7).
+template <class T, int NM, bool WEIGHTED, bool FULL>
+__device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
+                                            const T* __restrict__ cand, int Cb, int cc, int d, int wave,
+                                            int r, int h, const T* muiL, int msE) {
+  Frag<T> bc[2][NM];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int c = min(cc + ct * 32 + r, Cb - 1);
+    const T* crow = cand + (size_t)c * d + 16 * h;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) frag_load(bc[ct][m], crow + (wave + kWaves * m) * 32);
+  }
+  Frag<T> am[NM];
+  if constexpr (FULL) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) frag_load(am[m], muiL + r * msE + (wave + kWaves * m) * 32 + 16 * h);
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    lg[ct] = zero16();
+    mt[ct] = zero16();
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      if constexpr (WEIGHTED) mma_slab<T>(lg[ct], xf[m], bc[ct][m]);
+      if constexpr (FULL) mma_slab<T>(mt[ct], am[m], bc[ct][m]);
+    }
+  }
+}
+
+template <class T, bool WEIGHTED, bool FULL>
+__device__ __forceinline__ void s6_dispatch(int nm, f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
+                                            const T* cand, int Cb, int cc, int d, int wave, int r, int h,
+                                            const T* muiL, int msE) {
+  if (nm == 3) s6_products<T, 3, WEIGHTED, FULL>(lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+  else if (nm == 2) s6_products<T, 2, WEIGHTED, FULL>(lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+  else if (nm == 1) s6_products<T, 1, WEIGHTED, FULL>(lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+}
+
+// one 32x32 accumulator tile -> rows [c][k] of a partial slab (4 x 16-byte stores per lane):
+// register e of lane (r=c, h) is k = (e&3) + 8(e>>2) + 4h, so registers 4g..4g+3 are 4 contiguous k
+__device__ __forceinline__ void part_store(float* tile, const f32x16& a, int r, int h) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<float4*>(tile + r * kPartS + 8 * g + 4 * h) = float4{a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]};
+}
+__device__ __forceinline__ void part_add(float* tile, const f32x16& a, int r, int h) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float4* q = reinterpret_cast<float4*>(tile + r * kPartS + 8 * g + 4 * h);
+    const float4 v = *q;
+    *q = float4{v.x + a[4 * g], v.y + a[4 * g + 1], v.z + a[4 * g + 2], v.w + a[4 * g + 3]};
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
 // ---------------------------------------------------------------------------------------------
-template <class T, int MODE>
+template <class T, int MODE, int NS>
 __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kBf16 = sizeof(T) == 2;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int L = p.L, d = p.d, Dc = p.Dc, K = p.K;
-  const T* __restrict__ W1 = static_cast<const T*>(p.W1);
-  const T* __restrict__ Qc = static_cast<const T*>(p.Q);
-  const T* __restrict__ W2 = static_cast<const T*>(p.W2);
+  constexpr bool kDma = kBf16 && MODE == kFull;  // history staged in LDS by DMA
+  constexpr int PF = kBf16 ? 3 : 1;               // register prefetch depth of streamed weight slabs
+  // NS > 0: the embedding dim is a compile-time 32*NS and every slab loop fully unrolls
+  const int L = p.L, d = NS ? 32 * NS : p.d, Dc = p.Dc, K = p.K;
+  const int ns = d >> 5;
+  const int nct = n_ctiles(Dc);
+  const T* __restrict__ W1p = static_cast<const T*>(p.wp);
+  const T* __restrict__ Qp = W1p + w1p_elems(d, Dc);
+  const T* __restrict__ W2p = Qp + qp_elems(Dc);
   const bool weighted = (p.score_type == MINER_SCORE_WEIGHTED);
   const bool need_scores = (p.score_type != MINER_SCORE_NONE);
+  const int rowB = d * 2;
+  const int g16 = ((d >> 3) & 15) == 0;
+  char* ldsE = smem + p.offE;
+  T* muiL = reinterpret_cast<T*>(smem + p.offMui);        // [32][MS bytes]
+  const int msE = p.MS / (int)sizeof(T);
+  float* Lg = reinterpret_cast<float*>(smem + p.offLg);   // fp32 path: [32][kLgS], atomically summed
+  float* Mt = reinterpret_cast<float*>(smem + p.offMt);
+  float* part = reinterpret_cast<float*>(smem + p.offPart);  // bf16 path: 4 waves x kPartWave
+  constexpr int AwS = kBf16 ? 72 : 68;
 
-  T* muiL = reinterpret_cast<T*>(smem + p.offMui);   // [K_pad=32][MS bytes]
-  float* Lg = reinterpret_cast<float*>(smem + p.offLg);  // [32][kCChunk]
-  float* Mt = reinterpret_cast<float*>(smem + p.offMt);  // [32][kCChunk]
-  const int msE = p.MS / (int)sizeof(T);                 // mui row stride in elements
-
-  if constexpr (kBf16 && MODE == kFull) {
-    if (tid < 4) reinterpret_cast<u32x4*>(smem + p.offZ)[tid] = u32x4{0u, 0u, 0u, 0u};
+  {
+    FRESH_LANE_IDS();
+    if constexpr (kDma) {
+      if (tid < 4) reinterpret_cast<u32x4*>(smem + p.offZ)[tid] = u32x4{0u, 0u, 0u, 0u};
+      if (blockIdx.x < p.B)
+        dma_history(static_cast<const T*>(p.hist) + (size_t)blockIdx.x * L * d, L, d, ldsE, wave, lane);
+    }
+    if constexpr (!kBf16)
+      for (int i = tid; i < 2 * kMaxK * kLgS; i += kThreads) Lg[i] = 0.f;   // Lg and Mt are adjacent
   }
+  STAMP_DECL
+  int n_done = 0;
 
   for (int b = blockIdx.x; b < p.B; b += gridDim.x) {
+    ++n_done;
     const int cbase = p.cand_off ? p.cand_off[b] : b * p.C;
     const int Cb = p.cand_off ? (p.cand_off[b + 1] - cbase) : p.C;
     const T* __restrict__ cand = static_cast<const T*>(p.cand) + (size_t)cbase * d;
+    const int bnext = b + gridDim.x;
 
     if constexpr (MODE == kFull) {
       const T* __restrict__ E = static_cast<const T*>(p.hist) + (size_t)b * L * d;
-      float* S = reinterpret_cast<float*>(smem + p.offS);  // [32][kMaxL]
-      T* Aw = reinterpret_cast<T*>(smem + p.offAw);        // [32][AwS]
-      constexpr int AwS = kBf16 ? 72 : 68;
+      T* Ps = reinterpret_cast<T*>(smem + p.offP);         // P[l][c], row stride PS (aliases mui)
+      float* S = reinterpret_cast<float*>(smem + p.offS);  // Sᵀ[k][l], [32][kMaxL] (aliases mui)
+      T* Aw = reinterpret_cast<T*>(smem + p.offAw);        // A[k][l], [32][AwS]
 
-      // ---- S0: history -> LDS (bf16), zero S ------------------------------------------------
-      if constexpr (kBf16) {
-        const int per_row = d / 8;
-        const int n = L * per_row;
-        for (int i = tid; i < n; i += kThreads) {
-          const int row = i / per_row, c8 = i - row * per_row;
-          const u32x4 v = reinterpret_cast<const u32x4*>(E + (size_t)row * d)[c8];
-          *reinterpret_cast<u32x4*>(smem + p.offE + row * p.ES + c8 * 16) = v;
-        }
-      }
-      for (int i = tid; i < kMaxK * kMaxL; i += kThreads) S[i] = 0.f;
-      __syncthreads();
+      __syncthreads();  // history DMA landed (the barrier waits vmcnt(0)); last impression's LDS reads done
+      STAMP(0);
 
-      // ---- S1 + S2: Sᵀ += Q[:,ct] · tanh(W1[ct,:] · Eᵀ) -------------------------------------
+      // ---- S1: Pᵀ = tanh(W1[ct] · Eᵀ) -> P[l][c] in LDS -------------------------------------
       {
-        const int c0 = wave * 32;
-        if (c0 < Dc) {
-          const int nLt = (L + 31) >> 5;
+        FRESH_LANE_IDS();
+        if (wave < nct) {
           f32x16 acc0 = zero16(), acc1 = zero16();
-          const int crow = c0 + pi_row(r);
-          const bool cvalid = crow < Dc;
-          const T* w1row = W1 + (size_t)(cvalid ? crow : 0) * d + 16 * h;
-          const int l0 = r, l1 = 32 + r;
-          Frag<T> an;
-          if (cvalid) frag_load(an, w1row); else frag_zero(an);
-          for (int kb = 0; kb < d; kb += 32) {
-            Frag<T> a = an, b0, b1;
-            if (cvalid && kb + 32 < d) frag_load(an, w1row + kb + 32);
-            if constexpr (kBf16) {
-              if (l0 < L) frag_load(b0, reinterpret_cast<const T*>(smem + p.offE + l0 * p.ES) + kb + 16 * h);
-              else frag_zero(b0);
-              if (l1 < L) frag_load(b1, reinterpret_cast<const T*>(smem + p.offE + l1 * p.ES) + kb + 16 * h);
-              else frag_zero(b1);
-            } else {
-              if (l0 < L) frag_load(b0, E + (size_t)l0 * d + kb + 16 * h); else frag_zero(b0);
-              if (l1 < L) frag_load(b1, E + (size_t)l1 * d + kb + 16 * h); else frag_zero(b1);
+          const T* w1t = W1p + (size_t)wave * ns * 1024 + r * 32 + 16 * h;   // tile row r, slab 0
+          const int l0 = min(r, L - 1), l1 = min(32 + r, L - 1);  // rows >= L: finite, dropped in S3
+          Frag<T> ring[PF];
+#pragma unroll
+          for (int s = 0; s < PF; ++s) frag_load(ring[s], w1t + min(s, ns - 1) * 1024);
+          int j = 0;
+#pragma unroll
+          for (; j + PF <= ns; j += PF) {
+#pragma unroll
+            for (int s = 0; s < PF; ++s) {
+              const int kk = (j + s) * 32;
+              Frag<T> b0, b1;
+              if constexpr (kBf16) {
+                frag_load_E(b0, ldsE, l0, kk, h, rowB, g16);
+                frag_load_E(b1, ldsE, l1, kk, h, rowB, g16);
+              } else {
+                frag_load(b0, E + (size_t)l0 * d + kk + 16 * h);
+                frag_load(b1, E + (size_t)l1 * d + kk + 16 * h);
+              }
+              mma_slab<T>(acc0, ring[s], b0);
+              mma_slab<T>(acc1, ring[s], b1);
+              frag_load(ring[s], w1t + min(j + s + PF, ns - 1) * 1024);
+              __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
             }
-            mma_slab<T>(acc0, a, b0);
-            if (nLt > 1) mma_slab<T>(acc1, a, b1);
+          }
+#pragma unroll
+          for (int s = 0; s < PF; ++s) {
+            if (j + s < ns) {
+              const int kk = (j + s) * 32;
+              Frag<T> b0, b1;
+              if constexpr (kBf16) {
+                frag_load_E(b0, ldsE, l0, kk, h, rowB, g16);
+                frag_load_E(b1, ldsE, l1, kk, h, rowB, g16);
+              } else {
+                frag_load(b0, E + (size_t)l0 * d + kk + 16 * h);
+                frag_load(b1, E + (size_t)l1 * d + kk + 16 * h);
+              }
+              mma_slab<T>(acc0, ring[s], b0);
+              mma_slab<T>(acc1, ring[s], b1);
+            }
           }
 #pragma unroll
           for (int e = 0; e < 16; ++e) { acc0[e] = act_tanh<T>(acc0[e]); acc1[e] = act_tanh<T>(acc1[e]); }
-          // context codes: A operand rows k, contraction over this wave's 32 Dc columns
-          Frag<T> qa;
-          if (r < K) frag_load_pred(qa, Qc + (size_t)r * Dc, c0 + 16 * h, Dc); else frag_zero(qa);
+          // register e of lane (r=l, h) is c = 32*wave + 16h + e: 16 contiguous c of row l
           Frag<T> pf;
           acc_to_frag(pf, acc0);
-          f32x16 s0 = zero16();
-          mma_slab<T>(s0, qa, pf);
-#pragma unroll
-          for (int e = 0; e < 16; ++e) atomicAdd(&S[acc_row(e, h) * kMaxL + r], s0[e]);
-          if (nLt > 1) {
+          frag_store(Ps + r * p.PS + wave * 32 + 16 * h, pf);
+          if (L > 32) {
             acc_to_frag(pf, acc1);
-            f32x16 s1 = zero16();
-            mma_slab<T>(s1, qa, pf);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) atomicAdd(&S[acc_row(e, h) * kMaxL + 32 + r], s1[e]);
+            frag_store(Ps + (32 + r) * p.PS + wave * 32 + 16 * h, pf);
           }
         }
       }
       __syncthreads();
 
-      // ---- S3: masked softmax over the history ----------------------------------------------
+      // ---- S2: Sᵀ[k][l] = Σ_c Q[k][c] P[l][c]  (one wave per 32-position tile) ------------------
       {
+        FRESH_LANE_IDS();
+        if (wave * 32 < L) {
+          f32x16 acc = zero16();
+          const T* qrow = Qp + r * (nct * 32) + 16 * h;
+          const T* prow = Ps + (wave * 32 + r) * p.PS + 16 * h;
+          for (int j = 0; j < nct; ++j) {
+            Frag<T> qa, pb;
+            frag_load(qa, qrow + j * 32);
+            frag_load(pb, prow + j * 32);
+            mma_slab<T>(acc, qa, pb);
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) S[acc_row(e, h) * kMaxL + wave * 32 + r] = acc[e];
+        }
+      }
+      __syncthreads();
+      STAMP(1);
+
+      // ---- S3: masked softmax over the history (4 interests per wave, interleaved) ------------
+      {
+        FRESH_LANE_IDS();
         const int l = lane;
         const bool in = l < L;
         const bool real = in && p.mask[(size_t)b * L + l] != 0;
         const float bl = (p.bias && in) ? p.bias[(size_t)b * L + l] : 0.f;
+        constexpr int RK = kMaxK / kWaves;
+        float v[RK], m[RK], ex[RK], sum[RK];
 #pragma unroll
-        for (int kk = 0; kk < kMaxK / kWaves; ++kk) {
-          const int k = wave + kWaves * kk;
-          float v = in ? (real ? S[k * kMaxL + l] + bl : 1e-30f) : -INFINITY;
-          const float m = wave_max(v);
-          const float ex = in ? (kBf16 ? __expf(v - m) : expf(v - m)) : 0.f;
-          const float sum = wave_sum(ex);
-          const float a = (k < K) ? ex / sum : 0.f;
-          Aw[k * AwS + l] = from_f32<T>(a);
+        for (int q = 0; q < RK; ++q) {
+          const int k = wave + kWaves * q;
+          v[q] = in ? (real ? S[k * kMaxL + l] + bl : 1e-30f) : -INFINITY;   // model.py:180
+          m[q] = v[q];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+          for (int q = 0; q < RK; ++q) m[q] = fmaxf(m[q], __shfl_xor(m[q], o, 64));
+#pragma unroll
+        for (int q = 0; q < RK; ++q) { ex[q] = in ? act_exp<T>(v[q] - m[q]) : 0.f; sum[q] = ex[q]; }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+          for (int q = 0; q < RK; ++q) sum[q] += __shfl_xor(sum[q], o, 64);
+#pragma unroll
+        for (int q = 0; q < RK; ++q) {
+          const int k = wave + kWaves * q;
+          Aw[k * AwS + l] = from_f32<T>((k < K) ? ex[q] / sum[q] : 0.f);
         }
       }
       __syncthreads();
+      STAMP(2);
 
       // ---- S4: mui = A · E  (rows k, columns i) ---------------------------------------------
       {
+        FRESH_LANE_IDS();
         const int nLs = (L + 31) >> 5;
         Frag<T> af0, af1;
         frag_load(af0, Aw + r * AwS + 16 * h);
         if (nLs > 1) frag_load(af1, Aw + r * AwS + 32 + 16 * h); else frag_zero(af1);
-        const int nIt = d >> 5;
-        for (int it = wave; it < nIt; it += kWaves) {
+        for (int it = wave; it < ns; it += kWaves) {
           const int i0 = it * 32;
           f32x16 acc = zero16();
 #pragma unroll
@@ -322,31 +561,26 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
               Frag<T> bf;
               const int lb = ls * 32;
               if constexpr (kBf16) {
-                // E^T fragment via ds_read_b64_tr_b16: group g = lane>>4 reads 4 rows x 16 cols
+                // Eᵀ fragment via ds_read_b64_tr_b16: lane group g = lane>>4 reads 4 rows x 16 cols
                 const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
                 const int col = i0 + 16 * (g & 1) + 4 * pp;
+                const int ch = col >> 3, sub8 = (col & 7) * 2;
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
 #pragma unroll
                   for (int u = 0; u < 2; ++u) {
                     const int row = lb + 16 * (g >> 1) + 8 * s + 4 * u + q;
-                    const int off = (row < L) ? (p.offE + row * p.ES + col * 2) : p.offZ;
-                    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-                    typedef __attribute__((address_space(3))) char lds_char;
-                    const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_i16x4*)((lds_char*)smem + off));
-                    const unsigned lo = (unsigned)(unsigned short)v[0] | ((unsigned)(unsigned short)v[1] << 16);
-                    const unsigned hi = (unsigned)(unsigned short)v[2] | ((unsigned)(unsigned short)v[3] << 16);
-                    bf.q[s][2 * u] = lo;
-                    bf.q[s][2 * u + 1] = hi;
+                    const int off = (row < L) ? (p.offE + row * rowB + ((ch ^ eswz(row, g16)) << 4) + sub8) : p.offZ;
+                    const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)((lds_char*)smem + off));
+                    bf.q[s][2 * u] = (unsigned)(unsigned short)v[0] | ((unsigned)(unsigned short)v[1] << 16);
+                    bf.q[s][2 * u + 1] = (unsigned)(unsigned short)v[2] | ((unsigned)(unsigned short)v[3] << 16);
                   }
                 }
               } else {
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                  const int l = lb + 16 * h + e;
-                  const float v = (l < L) ? E[(size_t)l * d + i0 + r] : 0.f;
-                  bf.q[e >> 2][e & 3] = __float_as_uint(v);
+                for (int e = 0; e < 16; ++e) {   // rows >= L: finite data times a zero weight
+                  const int l = min(lb + 16 * h + e, L - 1);
+                  bf.q[e >> 2][e & 3] = __float_as_uint(E[(size_t)l * d + i0 + r]);
                 }
               }
               mma_slab<T>(acc, ls == 0 ? af0 : af1, bf);
@@ -360,10 +594,13 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           }
         }
       }
-      __syncthreads();
+      __syncthreads();  // history region free from here on
+      STAMP(3);
     } else {  // MODE == kTaa: multi_user_interest comes from global (query)
+      FRESH_LANE_IDS();
       const T* __restrict__ qy = static_cast<const T*>(p.hist) + (size_t)b * K * d;
       const int per_row = d * (int)sizeof(T) / 16;
+      __syncthreads();  // last impression's LDS reads done
       for (int i = tid; i < kMaxK * per_row; i += kThreads) {
         const int k = i / per_row, c = i - k * per_row;
         u32x4 v = u32x4{0u, 0u, 0u, 0u};
@@ -373,124 +610,186 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
       __syncthreads();
     }
 
-    if (!need_scores) continue;  // PolyAttention only (uniform branch; S4's barrier is behind us)
-
-    // ---- S5: X = gelu(W2 · muiᵀ), wave-owned d-tiles kept in registers -----------------------
-    const int nJt = d >> 5;
-    Frag<T> xf[kMaxJ];
-    if (weighted) {
-      f32x16 acc[kMaxJ];
-#pragma unroll
-      for (int m = 0; m < kMaxJ; ++m) acc[m] = zero16();
-      const T* w2row[kMaxJ];
-#pragma unroll
-      for (int m = 0; m < kMaxJ; ++m) {
-        const int jt = wave + kWaves * m;
-        w2row[m] = W2 + (size_t)((jt < nJt ? jt : 0) * 32 + pi_row(r)) * d + 16 * h;
-      }
-      const int nm = (nJt - wave + kWaves - 1) / kWaves;  // d-tiles owned by this wave
-      Frag<T> an[kMaxJ];
-#pragma unroll
-      for (int m = 0; m < kMaxJ; ++m) {
-        if (m < nm) frag_load(an[m], w2row[m]); else frag_zero(an[m]);
-      }
-      for (int kb = 0; kb < d; kb += 32) {
-        Frag<T> a[kMaxJ];
-#pragma unroll
-        for (int m = 0; m < kMaxJ; ++m) a[m] = an[m];
-        if (kb + 32 < d) {
-#pragma unroll
-          for (int m = 0; m < kMaxJ; ++m)
-            if (m < nm) frag_load(an[m], w2row[m] + kb + 32);
+    if (need_scores) {
+      // ---- S5: X = gelu(W2 · muiᵀ), wave-owned d-tiles kept in registers ---------------------
+      Frag<T> xf[kMaxJ];
+      {
+        FRESH_LANE_IDS();
+        const int nm = (ns - wave + kWaves - 1) / kWaves;
+        if (weighted) {
+          if (nm == 3) s5_gelu<T, PF, 3>(xf, W2p, muiL, msE, d, wave, r, h);
+          else if (nm == 2) s5_gelu<T, PF, 2>(xf, W2p, muiL, msE, d, wave, r, h);
+          else if (nm == 1) s5_gelu<T, PF, 1>(xf, W2p, muiL, msE, d, wave, r, h);
         }
-        Frag<T> bm;
-        frag_load(bm, muiL + r * msE + kb + 16 * h);
-#pragma unroll
-        for (int m = 0; m < kMaxJ; ++m)
-          if (m < nm) mma_slab<T>(acc[m], a[m], bm);
       }
-#pragma unroll
-      for (int m = 0; m < kMaxJ; ++m) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[m][e] = act_gelu<T>(acc[m][e]);
-        acc_to_frag(xf[m], acc[m]);
-      }
-    }
-    for (int i = tid; i < 2 * kMaxK * kCChunk; i += kThreads) Lg[i] = 0.f;  // Lg and Mt are adjacent
-    __syncthreads();
+      STAMP(4);
 
-    // ---- S6/S7 over candidate chunks ---------------------------------------------------------
-    for (int cc = 0; cc < Cb; cc += kCChunk) {
+      // ---- S6/S7 over candidate chunks ---------------------------------------------------------
+      for (int cc = 0; cc < Cb; cc += kCChunk) {
+        {
+          FRESH_LANE_IDS();
+          const int nm = (ns - wave + kWaves - 1) / kWaves;
+          f32x16 lg[2], mt[2];
+          lg[0] = lg[1] = mt[0] = mt[1] = zero16();
+          if (weighted) s6_dispatch<T, true, MODE == kFull>(nm, lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+          else s6_dispatch<T, false, MODE == kFull>(nm, lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+          if constexpr (kBf16) {
+            // two-round reduction through LDS with plain stores: waves 0-3 store, 4-7 add
+            float* slot = part + (wave & 3) * kPartWave;
+            if (wave < 4) {
+              part_store(slot, lg[0], r, h);
+              part_store(slot + kPartTile, lg[1], r, h);
+              part_store(slot + 2 * kPartTile, mt[0], r, h);
+              part_store(slot + 3 * kPartTile, mt[1], r, h);
+            }
+            __syncthreads();
+            if (wave >= 4) {
+              part_add(slot, lg[0], r, h);
+              part_add(slot + kPartTile, lg[1], r, h);
+              part_add(slot + 2 * kPartTile, mt[0], r, h);
+              part_add(slot + 3 * kPartTile, mt[1], r, h);
+            }
+          } else {
+            if (nm > 0) {
 #pragma unroll
-      for (int ct = 0; ct < kCChunk / 32; ++ct) {
-        const int c = cc + ct * 32 + r;
-        if (cc + ct * 32 < Cb) {
-          f32x16 lg = zero16(), mt = zero16();
-          const bool cvalid = c < Cb;
-          const T* crow = cand + (size_t)(cvalid ? c : 0) * d + 16 * h;
+              for (int ct = 0; ct < 2; ++ct) {
+                if (cc + ct * 32 < Cb) {
 #pragma unroll
-          for (int m = 0; m < kMaxJ; ++m) {
-            const int jt = wave + kWaves * m;
-            if (jt < nJt) {
-              Frag<T> bc;
-              if (cvalid) frag_load(bc, crow + jt * 32); else frag_zero(bc);
-              if (weighted) mma_slab<T>(lg, xf[m], bc);
-              if (MODE == kFull) {
-                Frag<T> am;
-                frag_load(am, muiL + r * msE + jt * 32 + 16 * h);
-                mma_slab<T>(mt, am, bc);
+                  for (int e = 0; e < 16; ++e) {
+                    const int k = acc_row(e, h);
+                    if (weighted) atomicAdd(&Lg[k * kLgS + ct * 32 + r], lg[ct][e]);
+                    if (MODE == kFull) atomicAdd(&Mt[k * kLgS + ct * 32 + r], mt[ct][e]);
+                  }
+                }
               }
             }
           }
-          if (wave < nJt) {
+        }
+        __syncthreads();
+        STAMP(5);
+        // S7: 8 lanes per candidate, 4 interests per lane
+        {
+          FRESH_LANE_IDS();
+          const int cl = tid >> 3, sub = tid & 7;
+          const int c = cc + cl;
+          const bool cval = c < Cb;
+          float lgv[4], mtv[4];
+          if constexpr (kBf16) {
+            const int ct = cl >> 5, cr = cl & 31;
+            float4 a = float4{0.f, 0.f, 0.f, 0.f}, mm = a;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              const int k = acc_row(e, h);
-              if (weighted) atomicAdd(&Lg[k * kCChunk + ct * 32 + r], lg[e]);
-              if (MODE == kFull) atomicAdd(&Mt[k * kCChunk + ct * 32 + r], mt[e]);
+            for (int w = 0; w < 4; ++w) {
+              const float* slot = part + w * kPartWave + cr * kPartS + 4 * sub;
+              const float4 x = *reinterpret_cast<const float4*>(slot + ct * kPartTile);
+              const float4 y = *reinterpret_cast<const float4*>(slot + (2 + ct) * kPartTile);
+              a = float4{a.x + x.x, a.y + x.y, a.z + x.z, a.w + x.w};
+              mm = float4{mm.x + y.x, mm.y + y.y, mm.z + y.z, mm.w + y.w};
+            }
+            lgv[0] = a.x; lgv[1] = a.y; lgv[2] = a.z; lgv[3] = a.w;
+            mtv[0] = mm.x; mtv[1] = mm.y; mtv[2] = mm.z; mtv[3] = mm.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int k = 4 * sub + j;
+              lgv[j] = Lg[k * kLgS + cl];
+              mtv[j] = Mt[k * kLgS + cl];
+              Lg[k * kLgS + cl] = 0.f;
+              Mt[k * kLgS + cl] = 0.f;
             }
           }
-        }
-      }
-      __syncthreads();
-      if (tid < kCChunk) {
-        const int c = cc + tid;
-        if (c < Cb) {
+          bool kv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int k = 4 * sub + j;
+            kv[j] = k < K;
+            if (MODE == kTaa) mtv[j] = (cval && kv[j]) ? p.value[(size_t)(cbase + c) * K + k] : 0.f;
+          }
           float sc;
-          if (MODE == kTaa) {
-            const float* val = p.value + (size_t)(cbase + c) * K;
+          if (weighted) {
             float mx = -INFINITY;
-            for (int k = 0; k < K; ++k) mx = fmaxf(mx, Lg[k * kCChunk + tid]);
-            float den = 0.f, num = 0.f;
-            for (int k = 0; k < K; ++k) {
-              const float ex = expf(Lg[k * kCChunk + tid] - mx);
-              den += ex;
-              num += ex * val[k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (kv[j]) mx = fmaxf(mx, lgv[j]);
+            mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+            float ex[4], den = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              ex[j] = kv[j] ? act_exp<T>(lgv[j] - mx) : 0.f;
+              den += ex[j];
             }
-            sc = num / den;
-          } else if (p.score_type == MINER_SCORE_WEIGHTED) {
-            float mx = -INFINITY;
-            for (int k = 0; k < K; ++k) mx = fmaxf(mx, Lg[k * kCChunk + tid]);
-            float den = 0.f;
-            for (int k = 0; k < K; ++k) den += expf(Lg[k * kCChunk + tid] - mx);
+            den += __shfl_xor(den, 1, 64);
+            den += __shfl_xor(den, 2, 64);
+            den += __shfl_xor(den, 4, 64);
             float acc = 0.f;
-            for (int k = 0; k < K; ++k) acc += (expf(Lg[k * kCChunk + tid] - mx) / den) * Mt[k * kCChunk + tid];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc += (ex[j] / den) * mtv[j];   // softmax weights · value
+            acc += __shfl_xor(acc, 1, 64);
+            acc += __shfl_xor(acc, 2, 64);
+            acc += __shfl_xor(acc, 4, 64);
             sc = acc;
           } else if (p.score_type == MINER_SCORE_MAX) {
             float mx = -INFINITY;
-            for (int k = 0; k < K; ++k) mx = fmaxf(mx, Mt[k * kCChunk + tid]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (kv[j]) mx = fmaxf(mx, mtv[j]);
+            mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
             sc = mx;
           } else {
             float s = 0.f;
-            for (int k = 0; k < K; ++k) s += Mt[k * kCChunk + tid];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s += kv[j] ? mtv[j] : 0.f;
+            s += __shfl_xor(s, 1, 64);
+            s += __shfl_xor(s, 2, 64);
+            s += __shfl_xor(s, 4, 64);
             sc = s / (float)K;
           }
-          p.scores[cbase + c] = sc;
+          if (sub == 0 && cval) p.scores[cbase + c] = sc;
         }
-        for (int k = 0; k < kMaxK; ++k) { Lg[k * kCChunk + tid] = 0.f; Mt[k * kCChunk + tid] = 0.f; }
+        __syncthreads();
+        STAMP(6);
       }
-      __syncthreads();
     }
+
+    if constexpr (kDma) {
+      FRESH_LANE_IDS();
+      if (bnext < p.B)   // the history region (and the partial slabs aliasing it) is free now
+        dma_history(static_cast<const T*>(p.hist) + (size_t)bnext * L * d, L, d, ldsE, wave, lane);
+    }
+    STAMP(7);
+  }
+  STAMP_FLUSH(n_done);
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight packing
+// ---------------------------------------------------------------------------------------------
+template <class T>
+__global__ void pack_weights_kernel(const T* __restrict__ W1, const T* __restrict__ Q, const T* __restrict__ W2,
+                                    int d, int Dc, int K, T* __restrict__ out) {
+  const size_t n1 = w1p_elems(d, Dc), nq = qp_elems(Dc), n2 = W2 ? w2p_elems(d) : 0;
+  const int ns = d >> 5, nct = n_ctiles(Dc);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n1 + nq + n2; i += (size_t)gridDim.x * blockDim.x) {
+    T v = (T)0.f;
+    if (i < n1) {
+      const size_t tile = i >> 10;
+      const int rr = (int)((i >> 5) & 31), cc = (int)(i & 31);
+      const int ct = (int)(tile / ns), j = (int)(tile % ns);
+      const int row = ct * 32 + pi_row(rr);
+      if (row < Dc) v = W1[(size_t)row * d + j * 32 + cc];
+    } else if (i < n1 + nq) {
+      const size_t q = i - n1;
+      const int k = (int)(q / (nct * 32)), c = (int)(q % (nct * 32));
+      if (k < K && c < Dc) v = Q[(size_t)k * Dc + c];
+    } else {
+      const size_t q = i - n1 - nq;
+      const size_t tile = q >> 10;
+      const int rr = (int)((q >> 5) & 31), cc = (int)(q & 31);
+      const int jt = (int)(tile / ns), j = (int)(tile % ns);
+      v = W2[(size_t)(jt * 32 + pi_row(rr)) * d + j * 32 + cc];
+    }
+    out[i] = v;
   }
 }
 
@@ -500,35 +799,46 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
 inline int round16(int x) { return (x + 15) & ~15; }
 
 struct Carve {
-  int ES, MS, offE, offZ, offLg, offMt, offMui, offS, offAw, total;
+  int MS, PS, offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, total;
 };
 
-Carve carve(int dtype, int mode, int L, int d) {
+// LDS carve (bytes).
+//   bf16 full:  [history image (partial slabs alias it after S4) | zero block | mui (P, S alias it
+//               before S4) | Aw]
+//   fp32 full:  [Lg Mt | mui (P, S alias) | Aw]
+//   bf16 TAA:   [partial slabs | mui];   fp32 TAA: [Lg Mt | mui]
+Carve carve(int dtype, int mode, int L, int d, int Dc) {
   Carve c{};
   const bool bf = dtype == MINER_DTYPE_BF16;
   const int es = bf ? 2 : 4;
-  const int lgmt = 2 * kMaxK * kCChunk * 4;
+  const int lgmt = 2 * kMaxK * kLgS * 4;
+  const int parts = 4 * kPartWave * 4;
   c.MS = d * es + 16;
-  if (mode == kFull && bf) {
-    c.ES = d * es + 16;
-    c.offE = 0;
-    c.offZ = round16(L * c.ES);
-    const int r1 = c.offZ + 64 > lgmt ? c.offZ + 64 : lgmt;  // Lg/Mt alias the history region
-    c.offLg = 0;
-    c.offMt = kMaxK * kCChunk * 4;
-    c.offMui = round16(r1);
-  } else {
-    c.ES = 0;
-    c.offE = 0;
-    c.offZ = 0;
-    c.offLg = 0;
-    c.offMt = kMaxK * kCChunk * 4;
-    c.offMui = lgmt;
-  }
-  const int r2 = 32 * c.MS > kMaxK * kMaxL * 4 ? 32 * c.MS : kMaxK * kMaxL * 4;
-  c.offS = c.offMui;  // S lives in the mui region until S4 overwrites it
-  c.offAw = round16(c.offMui + r2);
+  c.PS = n_ctiles(Dc) * 32 + (bf ? 8 : 4);
+  const int pbytes = round16(64 * c.PS * es);
+  const int r2a = 32 * c.MS;
+  const int r2b = pbytes + kMaxK * kMaxL * 4;
+  const int r2 = round16(mode == kFull ? (r2a > r2b ? r2a : r2b) : r2a);
   const int aw = mode == kFull ? (bf ? 32 * 72 * 2 : 32 * 68 * 4) : 0;
+  int off = 0;
+  if (bf) {
+    const int eimg = mode == kFull ? (L * d * 2 + 1023) & ~1023 : 0;   // whole 1 KiB DMA blocks
+    c.offE = 0;
+    c.offPart = 0;
+    const int r1 = eimg > parts ? eimg : parts;
+    c.offZ = round16(r1);
+    off = c.offZ + (mode == kFull ? 64 : 0);
+    c.offLg = c.offMt = 0;
+  } else {
+    c.offE = c.offZ = c.offPart = 0;
+    c.offLg = 0;
+    c.offMt = kMaxK * kLgS * 4;
+    off = lgmt;
+  }
+  c.offMui = round16(off);
+  c.offP = c.offMui;                       // P lives in the mui region until S4 overwrites it
+  c.offS = c.offMui + pbytes;              // S too
+  c.offAw = round16(c.offMui + r2);
   c.total = c.offAw + aw;
   return c;
 }
@@ -538,8 +848,9 @@ int check_shape(int dtype, int mode, int L, int d, int Dc, int K) {
   if (d <= 0 || K <= 0) return MINER_EINVAL;
   if (mode == kFull && (L <= 0 || Dc <= 0)) return MINER_EINVAL;
   if (K > kMaxK || d % 32 != 0 || d > kMaxD) return MINER_ESHAPE;
+  if (dtype == MINER_DTYPE_BF16 && mode == kFull && d % 64 != 0) return MINER_ESHAPE;
   if (mode == kFull && (L > kMaxL || Dc > kMaxDc)) return MINER_ESHAPE;
-  if (carve(dtype, mode, L, d).total > kLdsMax) return MINER_ELDS;
+  if (carve(dtype, mode, L, d, mode == kFull ? Dc : 1).total > kLdsMax) return MINER_ELDS;
   return MINER_OK;
 }
 
@@ -556,9 +867,9 @@ int num_cus() {
 
 inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <class T, int MODE>
+template <class T, int MODE, int NS>
 int launch(void* stream, const Params& prm, int lds) {
-  auto kern = miner_fused<T, MODE>;
+  auto kern = miner_fused<T, MODE, NS>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   const int per_cu = kLdsMax / lds > 0 ? (kLdsMax / lds > 2 ? 2 : kLdsMax / lds) : 1;
@@ -570,70 +881,112 @@ int launch(void* stream, const Params& prm, int lds) {
 }
 
 int run(void* stream, int dtype, int mode, Params prm) {
-  const Carve c = carve(dtype, mode, prm.L, prm.d);
-  prm.ES = c.ES; prm.MS = c.MS; prm.offE = c.offE; prm.offZ = c.offZ; prm.offLg = c.offLg;
-  prm.offMt = c.offMt; prm.offMui = c.offMui; prm.offS = c.offS; prm.offAw = c.offAw;
-  if (dtype == MINER_DTYPE_BF16)
-    return mode == kFull ? launch<__bf16, kFull>(stream, prm, c.total) : launch<__bf16, kTaa>(stream, prm, c.total);
-  return mode == kFull ? launch<float, kFull>(stream, prm, c.total) : launch<float, kTaa>(stream, prm, c.total);
+#ifdef MINER_STAMPS
+  if (const char* e = getenv("MINER_DBG")) prm.dbg = atoi(e);
+#endif
+  const Carve c = carve(dtype, mode, prm.L, prm.d, prm.Dc);
+  prm.MS = c.MS; prm.PS = c.PS; prm.offE = c.offE; prm.offZ = c.offZ; prm.offP = c.offP; prm.offS = c.offS;
+  prm.offMui = c.offMui; prm.offAw = c.offAw; prm.offPart = c.offPart; prm.offLg = c.offLg; prm.offMt = c.offMt;
+  if (dtype == MINER_DTYPE_BF16) {
+    // bf16 kernels specialised on the embedding dim (d = 32*NS) so the slab loops fully unroll
+    switch (prm.d) {
+#define MINER_NS_CASE(ns) \
+  case 32 * ns: return mode == kFull ? launch<__bf16, kFull, ns>(stream, prm, c.total) : launch<__bf16, kTaa, ns>(stream, prm, c.total);
+      MINER_NS_CASE(2) MINER_NS_CASE(4) MINER_NS_CASE(6) MINER_NS_CASE(8) MINER_NS_CASE(12)
+      MINER_NS_CASE(16) MINER_NS_CASE(24)
+#undef MINER_NS_CASE
+      default:
+        return mode == kFull ? launch<__bf16, kFull, 0>(stream, prm, c.total) : launch<__bf16, kTaa, 0>(stream, prm, c.total);
+    }
+  }
+  return mode == kFull ? launch<float, kFull, 0>(stream, prm, c.total) : launch<float, kTaa, 0>(stream, prm, c.total);
+}
+
+size_t packed_bytes(int dtype, int d, int Dc) {
+  const size_t es = dtype == MINER_DTYPE_BF16 ? 2 : 4;
+  return (w1p_elems(d, Dc) + qp_elems(Dc) + w2p_elems(d)) * es;
 }
 
 }  // namespace
 
 extern "C" {
 
+size_t miner_packed_weights_bytes(int dtype, int d, int Dc, int K) {
+  if ((dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) || d <= 0 || d % 32 || Dc <= 0 || K <= 0 || K > kMaxK)
+    return 0;
+  return packed_bytes(dtype, d, Dc);
+}
+
+int miner_pack_weights(void* stream, int dtype, const void* w_poly, const void* context_codes, const void* w_target,
+                       int d, int Dc, int K, void* packed) {
+  if (dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) return MINER_EINVAL;
+  if (d <= 0 || Dc <= 0 || K <= 0) return MINER_EINVAL;
+  if (d % 32 || K > kMaxK || Dc > kMaxDc || d > kMaxD) return MINER_ESHAPE;
+  if (!w_poly || !context_codes || !packed) return MINER_EINVAL;
+  if (!aligned16(packed)) return MINER_EALIGN;
+  const size_t n = w1p_elems(d, Dc) + qp_elems(Dc) + (w_target ? w2p_elems(d) : 0);
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  if (dtype == MINER_DTYPE_BF16)
+    hipLaunchKernelGGL(pack_weights_kernel<__bf16>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const __bf16*>(w_poly), static_cast<const __bf16*>(context_codes),
+                       static_cast<const __bf16*>(w_target), d, Dc, K, static_cast<__bf16*>(packed));
+  else
+    hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const float*>(w_poly), static_cast<const float*>(context_codes),
+                       static_cast<const float*>(w_target), d, Dc, K, static_cast<float*>(packed));
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
 int miner_score(void* stream, int dtype, int score_type, const void* history, const uint8_t* his_mask,
                 const float* his_bias, const void* candidates, const int32_t* cand_offsets,
-                const void* w_poly, const void* context_codes, const void* w_target, int B, int L, int C,
-                int d, int Dc, int K, float* scores, float* user_out) {
+                const void* packed_weights, int B, int L, int C, int d, int Dc, int K, float* scores,
+                float* user_out) {
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
   if (B < 0 || C < 0) return MINER_EINVAL;
   const int sh = check_shape(dtype, kFull, L, d, Dc, K);
   if (sh != MINER_OK) return sh;
-  if (!history || !his_mask || !w_poly || !context_codes) return MINER_EINVAL;
+  if (!history || !his_mask || !packed_weights) return MINER_EINVAL;
   if (score_type != MINER_SCORE_NONE && (!candidates || !scores)) return MINER_EINVAL;
-  if (score_type == MINER_SCORE_WEIGHTED && !w_target) return MINER_EINVAL;
   if (score_type == MINER_SCORE_NONE && !user_out) return MINER_EINVAL;
-  if (!aligned16(history) || !aligned16(candidates) || !aligned16(w_poly) || !aligned16(w_target))
-    return MINER_EALIGN;
+  if (!aligned16(history) || !aligned16(candidates) || !aligned16(packed_weights)) return MINER_EALIGN;
   if (B == 0) return MINER_OK;
   Params prm{};
   prm.hist = history; prm.mask = his_mask; prm.bias = his_bias; prm.cand = candidates;
-  prm.cand_off = cand_offsets; prm.W1 = w_poly; prm.Q = context_codes; prm.W2 = w_target;
-  prm.value = nullptr; prm.scores = scores; prm.mui_out = user_out;
+  prm.cand_off = cand_offsets; prm.wp = packed_weights; prm.value = nullptr; prm.scores = scores;
+  prm.mui_out = user_out;
   prm.B = B; prm.L = L; prm.C = C; prm.d = d; prm.Dc = Dc; prm.K = K; prm.score_type = score_type;
   return run(stream, dtype, kFull, prm);
 }
 
 int miner_target_aware(void* stream, int dtype, const void* query, const void* key, const float* value,
-                       const int32_t* cand_offsets, const void* w_target, int B, int C, int d, int K,
+                       const int32_t* cand_offsets, const void* packed_weights, int Dc, int B, int C, int d, int K,
                        float* out) {
-  if (B < 0 || C < 0) return MINER_EINVAL;
+  if (B < 0 || C < 0 || Dc <= 0) return MINER_EINVAL;
   const int sh = check_shape(dtype, kTaa, 1, d, 1, K);
   if (sh != MINER_OK) return sh;
-  if (!query || !key || !value || !w_target || !out) return MINER_EINVAL;
-  if (!aligned16(query) || !aligned16(key) || !aligned16(w_target)) return MINER_EALIGN;
+  if (!query || !key || !value || !packed_weights || !out) return MINER_EINVAL;
+  if (!aligned16(query) || !aligned16(key) || !aligned16(packed_weights)) return MINER_EALIGN;
   if (B == 0) return MINER_OK;
   Params prm{};
   prm.hist = query; prm.mask = nullptr; prm.bias = nullptr; prm.cand = key; prm.cand_off = cand_offsets;
-  prm.W1 = nullptr; prm.Q = nullptr; prm.W2 = w_target; prm.value = value; prm.scores = out;
-  prm.mui_out = nullptr; prm.B = B; prm.L = 1; prm.C = C; prm.d = d; prm.Dc = 1; prm.K = K;
-  prm.score_type = MINER_SCORE_WEIGHTED;
+  prm.wp = packed_weights; prm.value = value; prm.scores = out; prm.mui_out = nullptr;
+  prm.B = B; prm.L = 1; prm.C = C; prm.d = d; prm.Dc = Dc; prm.K = K; prm.score_type = MINER_SCORE_WEIGHTED;
   return run(stream, dtype, kTaa, prm);
 }
 
 int miner_supported(int dtype, int L, int d, int Dc, int K) { return check_shape(dtype, kFull, L, d, Dc, K); }
 
-int miner_lds_bytes(int dtype, int score_type, int L, int d) {
+int miner_lds_bytes(int dtype, int score_type, int L, int d, int Dc) {
   (void)score_type;
-  return carve(dtype, kFull, L, d).total;
+  return carve(dtype, kFull, L, d, Dc).total;
 }
 
 const char* miner_strerror(int code) {
   switch (code) {
     case MINER_OK: return "ok";
     case MINER_EINVAL: return "invalid argument (null pointer, bad enum or non-positive size)";
-    case MINER_ESHAPE: return "shape not supported by this build (K<=32, L<=64, Dc<=256, d%32==0, d<=768)";
+    case MINER_ESHAPE: return "shape not supported by this build (K<=32, L<=64, Dc<=256, d%32==0 (bf16: d%64==0), d<=768)";
     case MINER_EALIGN: return "device pointer not 16-byte aligned";
     case MINER_ELDS: return "shape needs more LDS than one CU has (160 KiB)";
     default: return code > 0 ? hipGetErrorString(static_cast<hipError_t>(code)) : "unknown error";
@@ -641,5 +994,18 @@ const char* miner_strerror(int code) {
 }
 
 int miner_abi_version(void) { return MINER_ABI_VERSION; }
+
+#ifdef MINER_STAMPS
+// diagnostic build only: read (and reset) the per-stage cycle sums; out[0..7] cycles, out[8] impressions
+int miner_debug_stage_cycles(unsigned long long* out) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), 8 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_stage_imps), sizeof(unsigned long long));
+  unsigned long long z[16] = {0};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, 16 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_imps), z, sizeof(unsigned long long));
+  return (int)e;
+}
+#endif
 
 }  // extern "C"

@@ -39,21 +39,25 @@ def pairwise_cosine_similarity(x: Tensor, y: Tensor, zero_diagonal: bool = False
     return dist
 
 
-class _WeightCache:
-    """Per-dtype contiguous copies of parameters, refreshed when a parameter changes."""
+class _PackCache:
+    """miner_pack_weights() output per (dtype, device), re-packed when a parameter changes
+    (tracked through the parameters' version counters and storage pointers)."""
 
     def __init__(self):
         self._c = {}
 
-    def get(self, p: Tensor, dtype: torch.dtype) -> Tensor:
-        key = (id(p), dtype, p.device)
-        ver = p._version
+    def get(self, dtype: torch.dtype, w_poly: Tensor, context_codes: Tensor, w_target: Tensor = None):
+        params = [t for t in (w_poly, context_codes, w_target) if t is not None]
+        key = (dtype, w_poly.device)
+        stamp = tuple((t._version, t.data_ptr()) for t in params)
         hit = self._c.get(key)
-        if hit is not None and hit[0] == ver and hit[1].data_ptr() == p.data_ptr():
-            return hit[2]
-        t = p.detach().to(dtype).contiguous()
-        self._c[key] = (ver, p, t)
-        return t
+        if hit is not None and hit[0] == stamp:
+            return hit[1]
+        with torch.no_grad():
+            packed = ops.pack_weights(w_poly.detach(), context_codes.detach(),
+                                      None if w_target is None else w_target.detach(), dtype=dtype)
+        self._c[key] = (stamp, packed)
+        return packed
 
 
 class PolyAttention(nn.Module):
@@ -65,15 +69,15 @@ class PolyAttention(nn.Module):
         self.context_codes = nn.Parameter(nn.init.xavier_uniform_(
             torch.empty(num_context_codes, context_code_dim), gain=nn.init.calculate_gain('tanh')))
         self.precision = "fp32"
-        self._wc = _WeightCache()
+        self._pc = _PackCache()
 
     def forward(self, embeddings: Tensor, attn_mask: Tensor, bias: Tensor = None) -> Tensor:
         """embeddings [B,L,d], attn_mask [B,L] bool, bias [B,L,C] (or [B,L]) -> [B,K,d] fp32."""
         dt = _PREC[self.precision]
         if bias is not None and bias.dim() == 3:
             bias = bias.mean(dim=2)                                  # model.py:176
-        return ops.poly_attention(embeddings.to(dt), attn_mask, self._wc.get(self.linear.weight, dt),
-                                  self._wc.get(self.context_codes, dt), his_bias=bias)
+        packed = self._pc.get(dt, self.linear.weight, self.context_codes)
+        return ops.poly_attention(embeddings.to(dt), attn_mask, packed, his_bias=bias)
 
 
 class TargetAwareAttention(nn.Module):
@@ -83,12 +87,17 @@ class TargetAwareAttention(nn.Module):
         super().__init__()
         self.linear = nn.Linear(in_features=embed_dim, out_features=embed_dim, bias=False)
         self.precision = "fp32"
-        self._wc = _WeightCache()
+        self._pc = _PackCache()
 
     def forward(self, query: Tensor, key: Tensor, value: Tensor) -> Tensor:
         """query [B,K,d], key [B,C,d], value [B,C,K] -> [B,C] fp32."""
         dt = _PREC[self.precision]
-        return ops.target_aware(query.to(dt), key.to(dt), value, self._wc.get(self.linear.weight, dt))
+        K, d = query.shape[1], query.shape[2]
+        if getattr(self, "_dummy", None) is None or self._dummy[0].shape != (32, d) or self._dummy[1].shape[0] != K \
+                or self._dummy[0].device != query.device:
+            self._dummy = (torch.zeros((32, d), device=query.device), torch.zeros((K, 32), device=query.device))
+        packed = self._pc.get(dt, self._dummy[0], self._dummy[1], self.linear.weight)
+        return ops.target_aware(query.to(dt), key.to(dt), value, packed)
 
 
 class Miner(nn.Module):
@@ -119,7 +128,7 @@ class Miner(nn.Module):
         if self.score_type == 'weighted':
             self.target_aware_attn = TargetAwareAttention(self.news_embed_dim)
         self.dropout = nn.Dropout(dropout)
-        self._wc = _WeightCache()
+        self._pc = _PackCache()
         self.set_precision(precision)
 
     def set_precision(self, precision: str) -> "Miner":
@@ -151,10 +160,9 @@ class Miner(nn.Module):
         dt = _PREC[self.precision]
         if category_bias is not None and category_bias.dim() == 3:
             category_bias = category_bias.mean(dim=2)                           # model.py:176
-        w2 = self._wc.get(self.target_aware_attn.linear.weight, dt) if self.score_type == 'weighted' else None
-        out = ops.score(history_repr.to(dt), his_mask, candidate_repr.to(dt),
-                        self._wc.get(self.poly_attn.linear.weight, dt),
-                        self._wc.get(self.poly_attn.context_codes, dt), w2,
+        w2 = self.target_aware_attn.linear.weight if self.score_type == 'weighted' else None
+        packed = self._pc.get(dt, self.poly_attn.linear.weight, self.poly_attn.context_codes, w2)
+        out = ops.score(history_repr.to(dt), his_mask, candidate_repr.to(dt), packed,
                         score_type=self.score_type, cand_offsets=cand_offsets, his_bias=category_bias,
                         return_user=return_user)
         if return_user:

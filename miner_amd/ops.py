@@ -3,8 +3,13 @@
 PyTorch is plumbing here: it owns device memory and the current HIP stream; the arithmetic runs in
 libminer_hip.so. Every call enqueues on ``torch.cuda.current_stream()`` and returns without
 synchronising. Inputs must be device tensors: there is no CPU path.
+
+Weights go through ``pack_weights`` once (the kernel's tiled layout); ``score`` also accepts the
+raw ``(w_poly, context_codes, w_target)`` tensors and packs them on the fly.
 """
 from __future__ import annotations
+
+import dataclasses
 
 import torch
 
@@ -14,16 +19,12 @@ _DTYPES = {torch.float32: _lib.DTYPE_F32, torch.bfloat16: _lib.DTYPE_BF16}
 
 
 def _ptr(t):
-    return None if t is None else ctypes_ptr(t)
-
-
-def ctypes_ptr(t: torch.Tensor) -> int:
-    return t.data_ptr()
+    return None if t is None else t.data_ptr()
 
 
 def _require_device(*ts):
     for t in ts:
-        if t is not None and t.device.type != "cuda":
+        if t is not None and isinstance(t, torch.Tensor) and t.device.type != "cuda":
             raise RuntimeError("miner_amd ops run on the GPU only (got a tensor on %s); the scoring "
                                "path has no CPU fallback" % t.device)
 
@@ -36,11 +37,15 @@ def _contig(t, dtype=None):
     return t.contiguous()
 
 
-def _dtype_code(t: torch.Tensor) -> int:
+def _dtype_code(dtype: torch.dtype) -> int:
     try:
-        return _DTYPES[t.dtype]
+        return _DTYPES[dtype]
     except KeyError:
-        raise TypeError(f"unsupported dtype {t.dtype}: use float32 (parity) or bfloat16 (throughput)")
+        raise TypeError(f"unsupported dtype {dtype}: use float32 (parity) or bfloat16 (throughput)")
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
 
 
 def check_offsets(cand_offsets: torch.Tensor, B: int, N: int) -> None:
@@ -50,36 +55,90 @@ def check_offsets(cand_offsets: torch.Tensor, B: int, N: int) -> None:
         raise ValueError(f"cand_offsets must be a non-decreasing int32 [B+1] array from 0 to {N}")
 
 
+@dataclasses.dataclass
+class PackedWeights:
+    """miner_pack_weights() output: one device buffer holding W1, Q and W2 in the kernel layout."""
+    buf: torch.Tensor
+    dtype: torch.dtype
+    d: int
+    Dc: int
+    K: int
+    has_target: bool
+
+
+def pack_weights(w_poly: torch.Tensor, context_codes: torch.Tensor, w_target: torch.Tensor | None = None,
+                 dtype: torch.dtype | None = None) -> PackedWeights:
+    """Pack poly_attn.linear.weight [Dc,d], poly_attn.context_codes [K,Dc] and (optionally)
+    target_aware_attn.linear.weight [d,d] (model.py:155-157, :198) for the kernels."""
+    _require_device(w_poly, context_codes, w_target)
+    dtype = dtype or w_poly.dtype
+    dt = _dtype_code(dtype)
+    w1 = _contig(w_poly, dtype)
+    q = _contig(context_codes, dtype)
+    w2 = _contig(w_target, dtype)
+    Dc, d = w1.shape
+    K = q.shape[0]
+    if q.shape[1] != Dc:
+        raise ValueError(f"context_codes must be [K,{Dc}], got {tuple(q.shape)}")
+    if w2 is not None and tuple(w2.shape) != (d, d):
+        raise ValueError(f"w_target must be [{d},{d}], got {tuple(w2.shape)}")
+    nbytes = _lib.lib().miner_packed_weights_bytes(dt, d, Dc, K)
+    if nbytes == 0:
+        raise ValueError(f"weights d={d} Dc={Dc} K={K} not supported by this build")
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=w1.device)
+    with torch.cuda.device(w1.device):
+        rc = _lib.lib().miner_pack_weights(_stream(w1.device), dt, _ptr(w1), _ptr(q), _ptr(w2), d, Dc, K, _ptr(buf))
+    _lib.check(rc, "miner_pack_weights")
+    return PackedWeights(buf, dtype, d, Dc, K, w2 is not None)
+
+
+def _as_packed(w_poly, context_codes, w_target, dtype) -> PackedWeights:
+    if isinstance(w_poly, PackedWeights):
+        if w_poly.dtype != dtype:
+            raise TypeError(f"packed weights are {w_poly.dtype}, activations {dtype}")
+        return w_poly
+    return pack_weights(w_poly, context_codes, w_target, dtype=dtype)
+
+
 def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tensor,
-          w_poly: torch.Tensor, context_codes: torch.Tensor, w_target: torch.Tensor | None = None, *,
+          w_poly, context_codes: torch.Tensor | None = None, w_target: torch.Tensor | None = None, *,
           score_type: str = "weighted", cand_offsets: torch.Tensor | None = None,
           his_bias: torch.Tensor | None = None, return_user: bool = False,
           validate_offsets: bool = True):
     """Fused PolyAttention -> Cand·muiᵀ -> aggregation (src/model/model.py:113-138).
 
     history [B,L,d], his_mask [B,L] bool, candidates [B,C,d] (dense) or [N,d] with
-    cand_offsets [B+1] int32 (ragged). Weights in the activation dtype (float32 or bfloat16).
+    cand_offsets [B+1] int32 (ragged). ``w_poly`` is a PackedWeights, or the raw weight tensors are
+    passed as (w_poly, context_codes, w_target). Activations float32 (parity) or bfloat16.
     Returns scores ([B,C] dense / [N] ragged, fp32) and, if return_user, mui [B,K,d] fp32.
     """
     st = _lib.SCORE_TYPES.get(score_type)
     if st is None or st == _lib.SCORE_NONE:
         raise ValueError("Invalid method of aggregating matching score")  # model.py:136
-    _require_device(history, his_mask, candidates, w_poly, context_codes, w_target, cand_offsets, his_bias)
-    dt = _dtype_code(history)
+    _require_device(history, his_mask, candidates, context_codes, w_target, cand_offsets, his_bias)
+    if not isinstance(w_poly, PackedWeights):
+        _require_device(w_poly)
     tdt = history.dtype
+    dt = _dtype_code(tdt)
     history = _contig(history)
     candidates = _contig(candidates, tdt)
-    w_poly = _contig(w_poly, tdt)
-    context_codes = _contig(context_codes, tdt)
-    w_target = _contig(w_target, tdt) if st == _lib.SCORE_WEIGHTED else None
-    if st == _lib.SCORE_WEIGHTED and w_target is None:
-        raise ValueError("score_type='weighted' needs w_target (target_aware_attn.linear.weight)")
     B, L, d = history.shape
-    K, Dc = context_codes.shape
-    if tuple(w_poly.shape) != (Dc, d):
-        raise ValueError(f"w_poly must be [{Dc},{d}], got {tuple(w_poly.shape)}")
-    if w_target is not None and tuple(w_target.shape) != (d, d):
-        raise ValueError(f"w_target must be [{d},{d}]")
+    if isinstance(w_poly, PackedWeights):
+        Dc, K = w_poly.Dc, w_poly.K
+    else:
+        K, Dc = context_codes.shape
+        if tuple(w_poly.shape) != (Dc, d):
+            raise ValueError(f"w_poly must be [{Dc},{d}], got {tuple(w_poly.shape)}")
+    code = _lib.lib().miner_supported(dt, L, d, Dc, K)
+    if code != 0:
+        raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
+    if st == _lib.SCORE_WEIGHTED and not isinstance(w_poly, PackedWeights) and w_target is None:
+        raise ValueError("score_type='weighted' needs w_target (target_aware_attn.linear.weight)")
+    pw = _as_packed(w_poly, context_codes, w_target if st == _lib.SCORE_WEIGHTED else None, tdt)
+    if pw.d != d:
+        raise ValueError(f"packed weights are for d={pw.d}, history has d={d}")
+    if st == _lib.SCORE_WEIGHTED and not pw.has_target:
+        raise ValueError("score_type='weighted' needs weights packed with w_target")
     mask = _contig(his_mask)
     if mask.dtype != torch.bool:
         mask = mask != 0
@@ -104,30 +163,25 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
             check_offsets(offs, B, candidates.shape[0])
         C = 0
         scores = torch.empty((candidates.shape[0],), device=history.device, dtype=torch.float32)
-    code = _lib.lib().miner_supported(dt, L, d, Dc, K)
-    if code != 0:
-        raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32) if return_user else None
-    stream = torch.cuda.current_stream(history.device).cuda_stream
     with torch.cuda.device(history.device):
-        rc = _lib.lib().miner_score(stream, dt, st, _ptr(history), _ptr(mask), _ptr(his_bias),
-                                    _ptr(candidates), _ptr(offs), _ptr(w_poly), _ptr(context_codes),
-                                    _ptr(w_target), B, L, C, d, Dc, K, _ptr(scores), _ptr(mui))
+        rc = _lib.lib().miner_score(_stream(history.device), dt, st, _ptr(history), _ptr(mask), _ptr(his_bias),
+                                    _ptr(candidates), _ptr(offs), _ptr(pw.buf), B, L, C, d, Dc, K,
+                                    _ptr(scores), _ptr(mui))
     _lib.check(rc, "miner_score")
     return (scores, mui) if return_user else scores
 
 
-def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly: torch.Tensor,
-                   context_codes: torch.Tensor, his_bias: torch.Tensor | None = None) -> torch.Tensor:
+def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly, context_codes: torch.Tensor | None = None,
+                   his_bias: torch.Tensor | None = None) -> torch.Tensor:
     """PolyAttention.forward (src/model/model.py:159-185) -> mui [B,K,d] fp32."""
-    _require_device(history, his_mask, w_poly, context_codes, his_bias)
-    dt = _dtype_code(history)
+    _require_device(history, his_mask, context_codes, his_bias)
     tdt = history.dtype
+    dt = _dtype_code(tdt)
     history = _contig(history)
-    w_poly = _contig(w_poly, tdt)
-    context_codes = _contig(context_codes, tdt)
+    pw = _as_packed(w_poly, context_codes, None, tdt)
     B, L, d = history.shape
-    K, Dc = context_codes.shape
+    Dc, K = pw.Dc, pw.K
     mask = _contig(his_mask)
     if mask.dtype != torch.bool:
         mask = mask != 0
@@ -138,29 +192,36 @@ def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly: torch.
     if code != 0:
         raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32)
-    stream = torch.cuda.current_stream(history.device).cuda_stream
     with torch.cuda.device(history.device):
-        rc = _lib.lib().miner_score(stream, dt, _lib.SCORE_NONE, _ptr(history), _ptr(mask), _ptr(his_bias),
-                                    None, None, _ptr(w_poly), _ptr(context_codes), None,
-                                    B, L, 0, d, Dc, K, None, _ptr(mui))
+        rc = _lib.lib().miner_score(_stream(history.device), dt, _lib.SCORE_NONE, _ptr(history), _ptr(mask),
+                                    _ptr(his_bias), None, None, _ptr(pw.buf), B, L, 0, d, Dc, K, None, _ptr(mui))
     _lib.check(rc, "miner_score(PolyAttention)")
     return mui
 
 
-def target_aware(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, w_target: torch.Tensor,
+def target_aware(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, w_target,
                  cand_offsets: torch.Tensor | None = None, validate_offsets: bool = True) -> torch.Tensor:
     """TargetAwareAttention.forward (src/model/model.py:200-216).
 
     query [B,K,d], key [B,C,d] (or [N,d] + cand_offsets), value [B,C,K] (or [N,K]) -> [B,C] / [N].
+    ``w_target`` is the [d,d] weight or a PackedWeights that holds it.
     """
-    _require_device(query, key, value, w_target, cand_offsets)
-    dt = _dtype_code(query)
+    _require_device(query, key, value, cand_offsets)
     tdt = query.dtype
+    dt = _dtype_code(tdt)
     query = _contig(query)
     key = _contig(key, tdt)
-    w_target = _contig(w_target, tdt)
     value = _contig(value, torch.float32)
     B, K, d = query.shape
+    if isinstance(w_target, PackedWeights):
+        pw = w_target
+        if not pw.has_target or pw.dtype != tdt:
+            raise ValueError("packed weights must hold w_target in the query dtype")
+    else:
+        _require_device(w_target)
+        # TAA alone needs only W2; pack it with a trivial (zero) PolyAttention block
+        pw = pack_weights(torch.zeros((32, d), device=query.device, dtype=tdt),
+                          torch.zeros((K, 32), device=query.device, dtype=tdt), w_target, dtype=tdt)
     if cand_offsets is None:
         C = key.shape[1]
         if tuple(key.shape) != (B, C, d) or tuple(value.shape) != (B, C, K):
@@ -173,9 +234,8 @@ def target_aware(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, w_
             check_offsets(offs, B, key.shape[0])
         C = 0
         out = torch.empty((key.shape[0],), device=query.device, dtype=torch.float32)
-    stream = torch.cuda.current_stream(query.device).cuda_stream
     with torch.cuda.device(query.device):
-        rc = _lib.lib().miner_target_aware(stream, dt, _ptr(query), _ptr(key), _ptr(value), _ptr(offs),
-                                           _ptr(w_target), B, C, d, K, _ptr(out))
+        rc = _lib.lib().miner_target_aware(_stream(query.device), dt, _ptr(query), _ptr(key), _ptr(value), _ptr(offs),
+                                           _ptr(pw.buf), pw.Dc, B, C, d, K, _ptr(out))
     _lib.check(rc, "miner_target_aware")
     return out

@@ -1,0 +1,74 @@
+"""Per-stage cycle breakdown of the fused kernel (diagnostic build with -DMINER_STAMPS).
+
+    python tools/stage_profile.py [--build] [--batch 8192] [--dtype bf16|f32]
+
+Thread 0 of each workgroup sums s_memtime deltas between the barriers that delimit the stages;
+reported as shader cycles per impression per workgroup (one workgroup per CU). Read the SHARES:
+the stamps themselves cost a few instructions per stage.
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+STAMP_LIB = os.path.join(ROOT, "miner_amd", "libminer_hip_stamps.so")
+STAGES = ["S0 wait history DMA", "S1+S2 W1/Q", "S3 softmax", "S4 A·E", "S5 W2+gelu", "S6 cand", "S7 score", "loop tail"]
+
+
+def build():
+    from miner_amd.build import hipcc, SRC, ARCH
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMINER_STAMPS",
+           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), SRC, "-o", STAMP_LIB]
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--L", type=int, default=50)
+    ap.add_argument("--d", type=int, default=768)
+    ap.add_argument("--C", type=int, default=40)
+    args = ap.parse_args()
+    if args.build:
+        build()
+        return
+    os.environ["MINER_HIP_LIB"] = STAMP_LIB
+    import torch
+    from miner_amd import _lib, ops, synthetic
+    h = _lib.lib()
+    fn = h.miner_debug_stage_cycles
+    fn.argtypes = [ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    imp = synthetic.impressions(36, 0, args.batch, L=args.L, d=args.d, C=args.C, device="cuda", dtype=dt)
+    W1, Q, W2 = synthetic.init_weights(36, args.d, 200, 32, device="cuda")
+    pw = ops.pack_weights(W1, Q, W2, dtype=dt)
+    for _ in range(2):
+        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+    torch.cuda.synchronize()
+    out = (ctypes.c_ulonglong * 16)()
+    fn(out)  # reset
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    reps = 3
+    for _ in range(reps):
+        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / reps
+    assert fn(out) == 0
+    n = out[8]
+    tot = sum(out[i] for i in range(8))
+    print(f"{args.dtype} L={args.L} d={args.d} C={args.C} batch={args.batch}: {ms:.3f} ms/launch, "
+          f"{n} impression-passes, {tot / n:.0f} cycles per impression per workgroup")
+    for i, name in enumerate(STAGES):
+        print(f"  {name:22s} {out[i] / n:10.0f} cycles  {100.0 * out[i] / tot:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
