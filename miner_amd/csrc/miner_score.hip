@@ -88,9 +88,13 @@ struct Params {
 
 // ---------------------------------------------------------------------------------------------
 // packed weight layout (elements of T):  [W1p | Qp | W2p]
-//   W1p: ceil(Dc/32) x (d/32) tiles of 32x32, tile (ct, j) row r = W1[32ct + pi(r)][32j .. 32j+31]
-//   Qp : 32 x 32*ceil(Dc/32), zero padded
-//   W2p: (d/32) x (d/32) tiles, tile (jt, j) row r = W2[32jt + pi(r)][32j .. 32j+31]
+//   W1p: ceil(Dc/32) x (d/32) blocks of 32x32 (block (ct, j) = rows 32ct + pi(r) of W1, columns
+//        32j .. 32j+31), zero padded past Dc;
+//   Qp : 32 x 32*ceil(Dc/32), row-major, zero padded;
+//   W2p: (d/32) x (d/32) blocks, block (jt, j) = rows 32jt + pi(r) of W2, columns 32j .. 32j+31.
+// Each block is stored FRAGMENT-MAJOR: 16-byte piece q of lane l = 32h + r sits at byte
+// (64q + l)*16 and holds columns 16h + q*(16/sizeof(T)) ... of row r — exactly what
+// frag_load_tile reads, so each wave-instruction reads 1 KiB contiguous (8 whole cache lines).
 // ---------------------------------------------------------------------------------------------
 __host__ __device__ inline int n_ctiles(int Dc) { return (Dc + 31) >> 5; }
 __host__ __device__ inline size_t w1p_elems(int d, int Dc) { return (size_t)n_ctiles(Dc) * (d >> 5) * 1024; }
@@ -118,6 +122,25 @@ __device__ __forceinline__ void frag_load(Frag<T>& f, const T* p) {
   const u32x4* s = reinterpret_cast<const u32x4*>(p);
 #pragma unroll
   for (int i = 0; i < kNQ<T>; ++i) f.q[i] = s[i];
+}
+
+// streamed-once data (candidate rows): non-temporal, so it does not evict the weights from L2
+#ifndef MINER_STREAM_NT
+#define MINER_STREAM_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void frag_load_stream(Frag<T>& f, const T* p) {
+  const u32x4* s = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = MINER_STREAM_NT ? __builtin_nontemporal_load(s + i) : s[i];
+}
+
+// slab fragment of a packed weight block (fragment-major, see the packed layout)
+template <class T>
+__device__ __forceinline__ void frag_load_tile(Frag<T>& f, const T* block, int lane) {
+  const u32x4* s = reinterpret_cast<const u32x4*>(block) + lane;
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = s[64 * i];
 }
 
 template <class T>
@@ -221,7 +244,7 @@ __device__ __forceinline__ void dma_history(const T* E, int L, int d, char* ldsE
     const int row = pos / cpr;
     const int c = pos - row * cpr;
     const T* src = (pos < total) ? E + (size_t)row * d + (size_t)((c ^ eswz(row, g16)) << 3) : E;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(ldsE + blk * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(ldsE + blk * 1024), 16, 0, MINER_STREAM_NT ? 2 : 0);
   }
 }
 
@@ -242,11 +265,13 @@ __device__ __forceinline__ void frag_load_E(Frag<__bf16>& f, const char* ldsE, i
 // that delimit it) into g_stage_cycles; p.dbg enables ablations.  Never in the product library.
 __device__ unsigned long long g_stage_cycles[16];
 __device__ unsigned long long g_stage_imps;
-#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define STAMP_DECL unsigned long long st_acc[12] = {0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
 #define STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } } while (0)
-#define STAMP_FLUSH(n) do { if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stage_cycles[i_], st_acc[i_]); atomicAdd(&g_stage_imps, (unsigned long long)(n)); } } while (0)
+#define STAMP_FLUSH(n) do { if (threadIdx.x == 0) { for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_stage_cycles[i_], st_acc[i_]); atomicAdd(&g_stage_imps, (unsigned long long)(n)); } } while (0)
 #define DBG(bit) (p.dbg & (1 << (bit)))
+#define STAMP_SYNC() __syncthreads()
 #else
+#define STAMP_SYNC() do {} while (0)
 #define STAMP_DECL
 #define STAMP(i) do {} while (0)
 #define STAMP_FLUSH(n) do {} while (0)
@@ -272,20 +297,21 @@ __device__ unsigned long long g_stage_imps;
 // from LDS.  The result stays in registers as slab fragments of the S6 contraction.
 template <class T, int PF, int NM>
 __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restrict__ W2p, const T* muiL,
-                                        int msE, int d, int wave, int r, int h) {
+                                        int msE, int d, int wave, int lane) {
   const int ns = d >> 5;
+  const int r = lane & 31, h = lane >> 5;
   f32x16 acc[NM];
   const T* w2t[NM];
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     acc[m] = zero16();
-    w2t[m] = W2p + (size_t)(wave + kWaves * m) * ns * 1024 + r * 32 + 16 * h;   // tile row r, slab 0
+    w2t[m] = W2p + (size_t)(wave + kWaves * m) * ns * 1024;   // block (tile, slab 0)
   }
   Frag<T> ring[PF][NM];
 #pragma unroll
   for (int s = 0; s < PF; ++s)
 #pragma unroll
-    for (int m = 0; m < NM; ++m) frag_load(ring[s][m], w2t[m] + min(s, ns - 1) * 1024);
+    for (int m = 0; m < NM; ++m) frag_load_tile(ring[s][m], w2t[m] + min(s, ns - 1) * 1024, lane);
   int j = 0;
 #pragma unroll
   for (; j + PF <= ns; j += PF) {
@@ -296,7 +322,7 @@ __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restric
 #pragma unroll
       for (int m = 0; m < NM; ++m) mma_slab<T>(acc[m], ring[s][m], bm);
 #pragma unroll
-      for (int m = 0; m < NM; ++m) frag_load(ring[s][m], w2t[m] + min(j + s + PF, ns - 1) * 1024);
+      for (int m = 0; m < NM; ++m) frag_load_tile(ring[s][m], w2t[m] + min(j + s + PF, ns - 1) * 1024, lane);
       __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
     }
   }
@@ -330,7 +356,7 @@ __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], co
     const int c = min(cc + ct * 32 + r, Cb - 1);
     const T* crow = cand + (size_t)c * d + 16 * h;
 #pragma unroll
-    for (int m = 0; m < NM; ++m) frag_load(bc[ct][m], crow + (wave + kWaves * m) * 32);
+    for (int m = 0; m < NM; ++m) frag_load_stream(bc[ct][m], crow + (wave + kWaves * m) * 32);
   }
   Frag<T> am[NM];
   if constexpr (FULL) {
@@ -382,7 +408,10 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kBf16 = sizeof(T) == 2;
   constexpr bool kDma = kBf16 && MODE == kFull;  // history staged in LDS by DMA
-  constexpr int PF = kBf16 ? 3 : 1;               // register prefetch depth of streamed weight slabs
+#ifndef MINER_PF
+#define MINER_PF 3
+#endif
+  constexpr int PF = kBf16 ? MINER_PF : 1;        // register prefetch depth of streamed weight slabs
   // NS > 0: the embedding dim is a compile-time 32*NS and every slab loop fully unrolls
   const int L = p.L, d = NS ? 32 * NS : p.d, Dc = p.Dc, K = p.K;
   const int ns = d >> 5;
@@ -419,7 +448,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
     ++n_done;
     const int cbase = p.cand_off ? p.cand_off[b] : b * p.C;
     const int Cb = p.cand_off ? (p.cand_off[b + 1] - cbase) : p.C;
-    const T* __restrict__ cand = static_cast<const T*>(p.cand) + (size_t)cbase * d;
+    const T* __restrict__ cand = static_cast<const T*>(p.cand) + (DBG(2) ? (size_t)0 : (size_t)cbase * d);
     const int bnext = b + gridDim.x;
 
     if constexpr (MODE == kFull) {
@@ -436,11 +465,11 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         FRESH_LANE_IDS();
         if (wave < nct) {
           f32x16 acc0 = zero16(), acc1 = zero16();
-          const T* w1t = W1p + (size_t)wave * ns * 1024 + r * 32 + 16 * h;   // tile row r, slab 0
+          const T* w1t = W1p + (size_t)wave * ns * 1024;   // block (tile, slab 0)
           const int l0 = min(r, L - 1), l1 = min(32 + r, L - 1);  // rows >= L: finite, dropped in S3
           Frag<T> ring[PF];
 #pragma unroll
-          for (int s = 0; s < PF; ++s) frag_load(ring[s], w1t + min(s, ns - 1) * 1024);
+          for (int s = 0; s < PF; ++s) frag_load_tile(ring[s], w1t + min(s, ns - 1) * 1024, lane);
           int j = 0;
 #pragma unroll
           for (; j + PF <= ns; j += PF) {
@@ -457,7 +486,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
               }
               mma_slab<T>(acc0, ring[s], b0);
               mma_slab<T>(acc1, ring[s], b1);
-              frag_load(ring[s], w1t + min(j + s + PF, ns - 1) * 1024);
+              frag_load_tile(ring[s], w1t + min(j + s + PF, ns - 1) * 1024, lane);
               __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
             }
           }
@@ -490,6 +519,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         }
       }
       __syncthreads();
+      STAMP(1);
 
       // ---- S2: Sᵀ[k][l] = Σ_c Q[k][c] P[l][c]  (one wave per 32-position tile) ------------------
       {
@@ -509,7 +539,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         }
       }
       __syncthreads();
-      STAMP(1);
+      STAMP(2);
 
       // ---- S3: masked softmax over the history (4 interests per wave, interleaved) ------------
       {
@@ -543,7 +573,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         }
       }
       __syncthreads();
-      STAMP(2);
+      STAMP(3);
 
       // ---- S4: mui = A · E  (rows k, columns i) ---------------------------------------------
       {
@@ -595,7 +625,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         }
       }
       __syncthreads();  // history region free from here on
-      STAMP(3);
+      STAMP(4);
     } else {  // MODE == kTaa: multi_user_interest comes from global (query)
       FRESH_LANE_IDS();
       const T* __restrict__ qy = static_cast<const T*>(p.hist) + (size_t)b * K * d;
@@ -617,12 +647,13 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         FRESH_LANE_IDS();
         const int nm = (ns - wave + kWaves - 1) / kWaves;
         if (weighted) {
-          if (nm == 3) s5_gelu<T, PF, 3>(xf, W2p, muiL, msE, d, wave, r, h);
-          else if (nm == 2) s5_gelu<T, PF, 2>(xf, W2p, muiL, msE, d, wave, r, h);
-          else if (nm == 1) s5_gelu<T, PF, 1>(xf, W2p, muiL, msE, d, wave, r, h);
+          if (nm == 3) s5_gelu<T, PF, 3>(xf, W2p, muiL, msE, d, wave, lane);
+          else if (nm == 2) s5_gelu<T, PF, 2>(xf, W2p, muiL, msE, d, wave, lane);
+          else if (nm == 1) s5_gelu<T, PF, 1>(xf, W2p, muiL, msE, d, wave, lane);
         }
       }
-      STAMP(4);
+      STAMP_SYNC();
+      STAMP(5);
 
       // ---- S6/S7 over candidate chunks ---------------------------------------------------------
       for (int cc = 0; cc < Cb; cc += kCChunk) {
@@ -633,17 +664,19 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           lg[0] = lg[1] = mt[0] = mt[1] = zero16();
           if (weighted) s6_dispatch<T, true, MODE == kFull>(nm, lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
           else s6_dispatch<T, false, MODE == kFull>(nm, lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+          STAMP_SYNC();
+          STAMP(6);
           if constexpr (kBf16) {
             // two-round reduction through LDS with plain stores: waves 0-3 store, 4-7 add
             float* slot = part + (wave & 3) * kPartWave;
-            if (wave < 4) {
+            if (wave < 4 && !DBG(3)) {
               part_store(slot, lg[0], r, h);
               part_store(slot + kPartTile, lg[1], r, h);
               part_store(slot + 2 * kPartTile, mt[0], r, h);
               part_store(slot + 3 * kPartTile, mt[1], r, h);
             }
             __syncthreads();
-            if (wave >= 4) {
+            if (wave >= 4 && !DBG(3)) {
               part_add(slot, lg[0], r, h);
               part_add(slot + kPartTile, lg[1], r, h);
               part_add(slot + 2 * kPartTile, mt[0], r, h);
@@ -666,7 +699,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           }
         }
         __syncthreads();
-        STAMP(5);
+        STAMP(7);
         // S7: 8 lanes per candidate, 4 interests per lane
         {
           FRESH_LANE_IDS();
@@ -748,16 +781,16 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           if (sub == 0 && cval) p.scores[cbase + c] = sc;
         }
         __syncthreads();
-        STAMP(6);
+        STAMP(8);
       }
     }
 
     if constexpr (kDma) {
       FRESH_LANE_IDS();
-      if (bnext < p.B)   // the history region (and the partial slabs aliasing it) is free now
+      if (bnext < p.B && !DBG(4))   // the history region (and the partial slabs aliasing it) is free now
         dma_history(static_cast<const T*>(p.hist) + (size_t)bnext * L * d, L, d, ldsE, wave, lane);
     }
-    STAMP(7);
+    STAMP(9);
   }
   STAMP_FLUSH(n_done);
 }
@@ -765,6 +798,16 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
 // ---------------------------------------------------------------------------------------------
 // weight packing
 // ---------------------------------------------------------------------------------------------
+// element x (0..1023) of a fragment-major block -> (tile row rr, column cc)
+template <class T>
+__device__ __forceinline__ void block_pos(int x, int& rr, int& cc) {
+  constexpr int epp = 16 / (int)sizeof(T);      // elements per 16-byte piece
+  const int piece = x / epp, t = x % epp;
+  const int q = piece >> 6, l = piece & 63;     // piece q of lane l
+  rr = l & 31;
+  cc = 16 * (l >> 5) + q * epp + t;
+}
+
 template <class T>
 __global__ void pack_weights_kernel(const T* __restrict__ W1, const T* __restrict__ Q, const T* __restrict__ W2,
                                     int d, int Dc, int K, T* __restrict__ out) {
@@ -774,7 +817,8 @@ __global__ void pack_weights_kernel(const T* __restrict__ W1, const T* __restric
     T v = (T)0.f;
     if (i < n1) {
       const size_t tile = i >> 10;
-      const int rr = (int)((i >> 5) & 31), cc = (int)(i & 31);
+      int rr, cc;
+      block_pos<T>((int)(i & 1023), rr, cc);
       const int ct = (int)(tile / ns), j = (int)(tile % ns);
       const int row = ct * 32 + pi_row(rr);
       if (row < Dc) v = W1[(size_t)row * d + j * 32 + cc];
@@ -785,7 +829,8 @@ __global__ void pack_weights_kernel(const T* __restrict__ W1, const T* __restric
     } else {
       const size_t q = i - n1 - nq;
       const size_t tile = q >> 10;
-      const int rr = (int)((q >> 5) & 31), cc = (int)(q & 31);
+      int rr, cc;
+      block_pos<T>((int)(q & 1023), rr, cc);
       const int jt = (int)(tile / ns), j = (int)(tile % ns);
       v = W2[(size_t)(jt * 32 + pi_row(rr)) * d + j * 32 + cc];
     }
@@ -996,11 +1041,11 @@ const char* miner_strerror(int code) {
 int miner_abi_version(void) { return MINER_ABI_VERSION; }
 
 #ifdef MINER_STAMPS
-// diagnostic build only: read (and reset) the per-stage cycle sums; out[0..7] cycles, out[8] impressions
+// diagnostic build only: read (and reset) the per-stage cycle sums; out[0..11] cycles, out[12] impressions
 int miner_debug_stage_cycles(unsigned long long* out) {
   hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), 8 * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_stage_imps), sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_cycles), 12 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 12, HIP_SYMBOL(g_stage_imps), sizeof(unsigned long long));
   unsigned long long z[16] = {0};
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_cycles), z, 16 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stage_imps), z, sizeof(unsigned long long));

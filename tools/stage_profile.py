@@ -15,29 +15,31 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 STAMP_LIB = os.path.join(ROOT, "miner_amd", "libminer_hip_stamps.so")
-STAGES = ["S0 wait history DMA", "S1+S2 W1/Q", "S3 softmax", "S4 A·E", "S5 W2+gelu", "S6 cand", "S7 score", "loop tail"]
+STAGES = ["S0 wait history DMA", "S1 W1·Eᵀ+tanh", "S2 Q·Pᵀ", "S3 softmax", "S4 A·E", "S5 W2+gelu", "S6 products", "S6 reduce", "S7 score", "loop tail"]
 
 
-def build():
+def build(extra=(), out=STAMP_LIB):
     from miner_amd.build import hipcc, SRC, ARCH
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMINER_STAMPS",
-           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), SRC, "-o", STAMP_LIB]
+           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), *extra, SRC, "-o", out]
     subprocess.run(cmd, check=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variant", default=None, help="build: -D flags, comma separated; run: library suffix")
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--L", type=int, default=50)
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--C", type=int, default=40)
     args = ap.parse_args()
+    lib = STAMP_LIB if not args.variant else STAMP_LIB.replace(".so", "_" + args.variant.replace(",", "_").replace("=", "") + ".so")
     if args.build:
-        build()
+        build(["-D" + x for x in args.variant.split(",")] if args.variant else (), lib)
         return
-    os.environ["MINER_HIP_LIB"] = STAMP_LIB
+    os.environ["MINER_HIP_LIB"] = lib
     import torch
     from miner_amd import _lib, ops, synthetic
     h = _lib.lib()
@@ -62,8 +64,8 @@ def main():
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / reps
     assert fn(out) == 0
-    n = out[8]
-    tot = sum(out[i] for i in range(8))
+    n = out[12]
+    tot = sum(out[i] for i in range(len(STAGES)))
     print(f"{args.dtype} L={args.L} d={args.d} C={args.C} batch={args.batch}: {ms:.3f} ms/launch, "
           f"{n} impression-passes, {tot / n:.0f} cycles per impression per workgroup")
     for i, name in enumerate(STAGES):
