@@ -240,6 +240,60 @@ def compute_metrics(pairs: GroupedPairs, metrics: List[str], save_result: bool =
 
 
 # ---------------------------------------------------------------------------------------------
+# evaluation loss on the batched layout
+# ---------------------------------------------------------------------------------------------
+
+
+def disagreement(mui: Tensor) -> Tensor:
+    """Per-impression mean pairwise cosine of the K interests, diagonal zeroed -> [B] fp32
+    (the ``pairwise_cosine_similarity(poly_attn, poly_attn, zero_diagonal=True)`` term of
+    src/loss.py:81; src/utils.py:9-29)."""
+    u = mui / torch.linalg.norm(mui, dim=2, keepdim=True)
+    g = torch.matmul(u, u.transpose(1, 2))
+    g.diagonal(dim1=1, dim2=2).zero_()
+    return g.mean(dim=(1, 2))
+
+
+def eval_loss_partials(mui: Tensor, scores: Tensor, labels: Tensor, *, first_sample: int, total_samples: int,
+                       cand_offsets: Tensor = None, batch_size: int = 32) -> Tensor:
+    """Numerator and positive count of the reference eval loss for a contiguous run of impressions.
+
+    The reference evaluates one sample per (impression, candidate), impression-major, in batches
+    of ``eval_batch_size`` (src/reader.py:376-379, config/eval_miner.txt:19) and sums
+    ``Loss.compute_eval_loss`` per batch (src/loss.py:68-85, src/trainer.py:276-291), so the batch
+    partition matters (a per-batch *mean* of the disagreement). Sample s (global index) lies in
+    batch s // batch_size of size n_b = min(batch_size, total - batch_size·(s // batch_size)); the
+    numerator is Σ_s D(imp(s)) / n_b(s) + Σ_s -logsigmoid(score_s)·label_s. Both sums decompose
+    over impression ranges, so ranks add their partials (``first_sample`` = the global index of
+    this run's first sample). Returns a float64 tensor [numerator, positives]; the loss is
+    numerator / positives.
+    """
+    dev = scores.device
+    if cand_offsets is None:
+        B, C = scores.shape
+        sizes = torch.full((B,), C, device=dev, dtype=torch.int64)
+    else:
+        sizes = torch.diff(cand_offsets.to(dev, torch.int64))
+    s = scores.reshape(-1).double()
+    lab = labels.reshape(-1).to(dev).double()
+    D = torch.repeat_interleave(disagreement(mui.float()).double(), sizes)
+    idx = first_sample + torch.arange(s.numel(), device=dev, dtype=torch.int64)
+    bstart = (idx // batch_size) * batch_size
+    nb = torch.clamp(total_samples - bstart, max=batch_size).double()
+    num = (D / nb).sum() + (-torch.nn.functional.logsigmoid(s) * lab).sum()
+    return torch.stack([num, lab.sum()])
+
+
+def eval_loss(mui: Tensor, scores: Tensor, labels: Tensor, cand_offsets: Tensor = None,
+              batch_size: int = 32) -> float:
+    """Single-process eval loss (src/trainer.py:291: total_loss / total_pos_example)."""
+    n = scores.numel()
+    p = eval_loss_partials(mui, scores, labels, first_sample=0, total_samples=n, cand_offsets=cand_offsets,
+                           batch_size=batch_size)
+    return float(p[0] / p[1])
+
+
+# ---------------------------------------------------------------------------------------------
 # evaluator classes (reference contract)
 # ---------------------------------------------------------------------------------------------
 
