@@ -193,12 +193,14 @@ def main():
     tflops = fl / (kern_ms / 1e3) / 1e12
     gbs = by / (kern_ms / 1e3) / 1e9
     traffic = load_traffic(args.traffic)
-    traffic_bytes = None
+    traffic_bytes, mfma_busy = None, None
     if traffic and traffic.get("batch") == B:
         traffic_bytes = traffic.get("hbm_bytes_per_launch")
+        mfma_busy = traffic.get("mfma_busy_frac")
     roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic_bytes,
-            "kernel": "miner_fused<bf16,full>", "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4)}
+            "kernel": "miner_fused<bf16,full>", "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4),
+            "mfma_busy_pmc": mfma_busy}
     roof_hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_launch": by,
                 "traffic": traffic_bytes}

@@ -1,0 +1,90 @@
+"""Fold rocprofv3 PMC passes over bench.py into profiles/pmc_traffic.json (read by bench.py).
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py ...
+    rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES -d gpurun_out/pmc_sq ...
+    python tools/pmc_traffic.py --batch 32768 gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_sq
+
+Per launch of the bf16 scoring kernel (miner_fused<bf16, full>): the median over dispatches of each
+counter (rows of one dispatch summed). HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB, and on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream
+(16 B/lane loads and LDS-DMA alike), so hbm = (2·FETCH_SIZE + WRITE_SIZE)·1024. MFMA busy =
+SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / XCDs · 4 SIMDs · CUs): GRBM_GUI_ACTIVE comes back
+as one row per XCC, so the per-dispatch sum is XCDs x the kernel's busy cycles.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL_TAG = "miner_fusedIDF16bLi0E"     # mangled miner_fused<__bf16, kFull, ...>
+
+
+def read_counters(d):
+    per = defaultdict(lambda: defaultdict(float))   # dispatch -> counter -> value
+    names = {}
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                kn = row.get("Kernel_Name", "")
+                if KERNEL_TAG not in kn and "miner_fused<__bf16, 0" not in kn:
+                    continue
+                did = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                per[did][row["Counter_Name"]] += float(row["Counter_Value"])
+                names[did] = kn
+    out = defaultdict(list)
+    for did, cs in per.items():
+        for c, v in cs.items():
+            out[c].append(v)
+    return {c: statistics.median(v) for c, v in out.items()}, len(per)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--batch", type=int, required=True)
+    ap.add_argument("--cus", type=int, default=256)
+    ap.add_argument("--xcds", type=int, default=8)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+    med, n = {}, {}
+    for d in args.dirs:
+        if not os.path.isdir(d):
+            continue
+        m, k = read_counters(d)
+        med.update(m)
+        n[d] = k
+    if "FETCH_SIZE" not in med or "WRITE_SIZE" not in med:
+        sys.exit(f"missing FETCH_SIZE/WRITE_SIZE for {KERNEL_TAG}: found {sorted(med)} ({n})")
+    fetch = 2 * med["FETCH_SIZE"] * 1024
+    write = med["WRITE_SIZE"] * 1024
+    res = {
+        "workload": "L50_K32_d768_Dc200_C40_bf16", "batch": args.batch, "kernel": "miner_fused<bf16,full>",
+        "dispatches": n, "FETCH_SIZE_KiB": med["FETCH_SIZE"], "WRITE_SIZE_KiB": med["WRITE_SIZE"],
+        "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
+        "hbm_bytes_per_launch": fetch + write,
+        "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count of 16B/lane streams), KiB -> bytes",
+    }
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in med and "GRBM_GUI_ACTIVE" in med:
+        res["SQ_VALU_MFMA_BUSY_CYCLES"] = med["SQ_VALU_MFMA_BUSY_CYCLES"]
+        res["GRBM_GUI_ACTIVE"] = med["GRBM_GUI_ACTIVE"]
+        gui = med["GRBM_GUI_ACTIVE"] / args.xcds
+        res["gpu_busy_cycles"] = gui
+        res["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui * 4 * args.cus)
+        res["mfma_instructions_32x32x16"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / 32
+    for c in ("SQ_BUSY_CU_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+        if c in med:
+            res[c] = med[c]
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
