@@ -4,14 +4,18 @@
 // impressions b = blockIdx.x, blockIdx.x + gridDim.x, ...  Everything between the HBM reads of an
 // impression's history/candidate rows and its fp32 score writes stays on chip:
 //
-//   S0  history rows E[L,d] -> LDS by LDS-DMA (bf16; the fp32 parity mode reads them from L2)
-//   S1  Pᵀ = tanh(W1 · Eᵀ)        [Dc,L]  MFMA, wave w owns Dc-tile w; P -> LDS   (model.py:171)
-//   S2  Sᵀ = Q · Pᵀ               [K,L]   MFMA, one wave per 32-position tile      (model.py:174)
-//   S3  A  = softmax_L(fill(Sᵀ))  [K,L]   wave shuffles; masked -> 1e-30           (model.py:178-181)
-//   S4  mui = A · E               [K,d]   MFMA, Eᵀ read with ds_read_b64_tr_b16    (model.py:182)
+//   S0  history rows E[L,d] + mask/bias -> LDS by LDS-DMA, issued during the previous impression
+//       (bf16; the fp32 parity mode reads them from L2)
+//   S1  Pᵀ = tanh(W1 · Eᵀ)        [Dc,L]  MFMA, wave w owns Dc-tile w                 (model.py:171)
+//   S2  S_w = P_w · Q_wᵀ          [L,K]   bf16: fused into S1's epilogue, the tanh'd accumulator
+//       is the A operand; per-wave partials -> LDS (fp32: separate stage)          (model.py:174)
+//   S3  A  = softmax_L(fill(S))   [K,L]   bf16: 16 lanes per interest, DPP row reductions;
+//       masked -> 1e-30                                                           (model.py:178-181)
+//   S4  muiᵀ = Eᵀ · Aᵀ            [d,K]   MFMA, Eᵀ read with ds_read_b64_tr_b16; the candidate
+//       rows are then DMA'd into the (dead) history image, landing during S5        (model.py:182)
 //   S5  X  = gelu(W2 · muiᵀ)      [d,K]   MFMA, wave w owns d-tiles w, w+8, w+16   (model.py:212)
-//   S6  Lgᵀ = Xᵀ·Candᵀ, Mᵀ = mui·Candᵀ  [K,C]  MFMA split over the waves' d-tiles,
-//       reduced through LDS with plain stores in two rounds                     (model.py:127,213)
+//   S6  Lgᵀ = Xᵀ·Candᵀ, Mᵀ = mui·Candᵀ  [K,C]  MFMA split over the waves' d-tiles, reduced
+//       through LDS with plain stores in two rounds; the next history DMA is issued here (model.py:127,213)
 //   S7  score_c = Σ_k softmax_K(Lg)_k · M_k  (or max_k / mean_k of M)      (model.py:128-134,213-214)
 //
 // Operand layout (both dtypes) — a "slab" is 32 consecutive contraction indices: lane
@@ -65,6 +69,8 @@ constexpr int kLgS = kCChunk + 1;      // fp32-path Lg/Mt row stride (floats)
 constexpr int kPartS = 36;             // bf16-path partial slab row stride (floats): [c][k] rows
 constexpr int kPartTile = 32 * kPartS; // one 32x32 tile, floats
 constexpr int kPartWave = 4 * kPartTile;  // Lg ct0, Lg ct1, Mt ct0, Mt ct1
+constexpr int kSPS = kMaxL + 4;        // bf16-path S-partial row stride (floats): [k][l] rows
+constexpr int kSPTile = kMaxK * kSPS;  // one wave's S partial (floats)
 
 enum Mode { kFull = 0, kTaa = 1 };
 
@@ -82,7 +88,8 @@ struct Params {
   // LDS carve (bytes)
   int MS;       // mui row stride
   int PS;       // P row stride (elements)
-  int offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt;
+  int offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux;
+  int eimg;     // bytes of the history image (bf16): the candidate rows may be staged there
   int dbg;      // ablation bits, honoured only by the -DMINER_STAMPS diagnostic build
 };
 
@@ -187,6 +194,24 @@ __device__ __forceinline__ void mma_slab(f32x16& acc, const Frag<T>& a, const Fr
 
 __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
 
+// all-reduce over the 16 lanes of a DPP row: quad_perm xor1, xor2, row_half_mirror, row_mirror
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row16_max(float x) {
+  x = fmaxf(x, dpp_f<0xB1>(x));
+  x = fmaxf(x, dpp_f<0x4E>(x));
+  x = fmaxf(x, dpp_f<0x141>(x));
+  return fmaxf(x, dpp_f<0x140>(x));
+}
+__device__ __forceinline__ float row16_sum(float x) {
+  x += dpp_f<0xB1>(x);
+  x += dpp_f<0x4E>(x);
+  x += dpp_f<0x141>(x);
+  return x + dpp_f<0x140>(x);
+}
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -233,18 +258,52 @@ __device__ __forceinline__ int eswz(int row, int g16) {
   return g16 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 1) << 2) | ((row >> 1) & 3));
 }
 
+__device__ __forceinline__ unsigned lds_offset(const void* p) { return (unsigned)(uintptr_t)(const lds_char*)p; }
+
+// LDS-DMA from inline asm.  hipcc tracks its own global_load_lds and then waits vmcnt(0) before
+// every later LDS access it cannot prove disjoint; an asm DMA is invisible to that analysis.  Its
+// completion is the consumer's business: an explicit `s_waitcnt vmcnt(0)` before the barrier that
+// publishes the data (vm_wait_all).  hipcc's own vmcnt(N) waits stay correct — an older untracked
+// load only makes the in-order counter wait for one more.  M0 (the LDS base of the DMA) is saved
+// and restored around the instruction.  `lds` must be wave-uniform; lane i writes lds + i·size.
+__device__ __forceinline__ void dma_b128(const void* g, unsigned lds) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_b32(const void* g, unsigned lds) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// nrows rows of d elements -> the swizzled image (whole 1 KiB blocks, one per wave-instruction)
 template <class T>
-__device__ __forceinline__ void dma_history(const T* E, int L, int d, char* ldsE, int wave, int lane) {
+__device__ __forceinline__ void dma_rows(const T* src, int nrows, int d, char* img, int wave, int lane) {
   const int cpr = d >> 3;                 // 16-byte chunks per row
   const int g16 = (cpr & 15) == 0;
-  const int total = L * cpr;
+  const int total = nrows * cpr;
   const int nblk = (total + 63) >> 6;
   for (int blk = wave; blk < nblk; blk += kWaves) {
     const int pos = blk * 64 + lane;
     const int row = pos / cpr;
     const int c = pos - row * cpr;
-    const T* src = (pos < total) ? E + (size_t)row * d + (size_t)((c ^ eswz(row, g16)) << 3) : E;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(ldsE + blk * 1024), 16, 0, MINER_STREAM_NT ? 2 : 0);
+    const T* g = (pos < total) ? src + (size_t)row * d + (size_t)((c ^ eswz(row, g16)) << 3) : src;
+    dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
+  }
+}
+
+// impression b's mask bytes (as the aligned words covering them) and fp32 bias -> the aux block
+__device__ __forceinline__ void dma_aux(const uint8_t* mask, const float* bias, int B, int L, int b, char* aux,
+                                        int wave, int lane) {
+  if (wave == 0) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(mask + (size_t)b * L) & ~(uintptr_t)3;
+    const uintptr_t last = reinterpret_cast<uintptr_t>(mask + (size_t)B * L - 1) & ~(uintptr_t)3;
+    const uintptr_t w = a + 4 * (uintptr_t)lane;
+    dma_b32(reinterpret_cast<const void*>(w < last ? w : last), __builtin_amdgcn_readfirstlane(lds_offset(aux)));
+  } else if (wave == 1 && bias) {
+    dma_b32(bias + (size_t)b * L + min(lane, L - 1), __builtin_amdgcn_readfirstlane(lds_offset(aux + 256)));
   }
 }
 
@@ -348,20 +407,40 @@ __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restric
 // row (finite data, never read back by S7).
 template <class T, int NM, bool WEIGHTED, bool FULL>
 __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
-                                            const T* __restrict__ cand, int Cb, int cc, int d, int wave,
-                                            int r, int h, const T* muiL, int msE) {
+                                            const Frag<T> (&amr)[kMaxJ], const T* __restrict__ cand,
+                                            const char* cimg, int Cb, int cc, int d, int wave, int r, int h,
+                                            const T* muiL, int msE) {
   Frag<T> bc[2][NM];
+  if constexpr (sizeof(T) == 2) {
+    if (cimg) {   // candidate rows DMA'd into the swizzled image during S5
+      const int g16 = ((d >> 3) & 15) == 0;
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    const int c = min(cc + ct * 32 + r, Cb - 1);
-    const T* crow = cand + (size_t)c * d + 16 * h;
+      for (int ct = 0; ct < 2; ++ct) {
+        const int c = min(cc + ct * 32 + r, Cb - 1);
 #pragma unroll
-    for (int m = 0; m < NM; ++m) frag_load_stream(bc[ct][m], crow + (wave + kWaves * m) * 32);
+        for (int m = 0; m < NM; ++m)
+          frag_load_E(reinterpret_cast<Frag<__bf16>&>(bc[ct][m]), cimg, c, (wave + kWaves * m) * 32, h, d * 2, g16);
+      }
+    }
   }
+  if (!cimg || sizeof(T) != 2) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int c = min(cc + ct * 32 + r, Cb - 1);
+      const T* crow = cand + (size_t)c * d + 16 * h;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) frag_load_stream(bc[ct][m], crow + (wave + kWaves * m) * 32);
+    }
+  }
+  // mui fragments of the wave's d-tiles: bf16 preloads them (amr) before the chunk loop, because
+  // the partial slabs overwrite mui; fp32 reads them here
   Frag<T> am[NM];
   if constexpr (FULL) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) frag_load(am[m], muiL + r * msE + (wave + kWaves * m) * 32 + 16 * h);
+    for (int m = 0; m < NM; ++m) {
+      if constexpr (sizeof(T) == 2) am[m] = amr[m];
+      else frag_load(am[m], muiL + r * msE + (wave + kWaves * m) * 32 + 16 * h);
+    }
   }
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
@@ -377,11 +456,11 @@ __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], co
 
 template <class T, bool WEIGHTED, bool FULL>
 __device__ __forceinline__ void s6_dispatch(int nm, f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
-                                            const T* cand, int Cb, int cc, int d, int wave, int r, int h,
-                                            const T* muiL, int msE) {
-  if (nm == 3) s6_products<T, 3, WEIGHTED, FULL>(lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
-  else if (nm == 2) s6_products<T, 2, WEIGHTED, FULL>(lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
-  else if (nm == 1) s6_products<T, 1, WEIGHTED, FULL>(lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+                                            const Frag<T> (&am)[kMaxJ], const T* cand, const char* cimg, int Cb,
+                                            int cc, int d, int wave, int r, int h, const T* muiL, int msE) {
+  if (nm == 3) s6_products<T, 3, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
+  else if (nm == 2) s6_products<T, 2, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
+  else if (nm == 1) s6_products<T, 1, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
 }
 
 // one 32x32 accumulator tile -> rows [c][k] of a partial slab (4 x 16-byte stores per lane):
@@ -435,8 +514,10 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
     FRESH_LANE_IDS();
     if constexpr (kDma) {
       if (tid < 4) reinterpret_cast<u32x4*>(smem + p.offZ)[tid] = u32x4{0u, 0u, 0u, 0u};
-      if (blockIdx.x < p.B)
-        dma_history(static_cast<const T*>(p.hist) + (size_t)blockIdx.x * L * d, L, d, ldsE, wave, lane);
+      if (blockIdx.x < p.B) {
+        dma_rows(static_cast<const T*>(p.hist) + (size_t)blockIdx.x * L * d, L, d, ldsE, wave, lane);
+        dma_aux(p.mask, p.bias, p.B, L, blockIdx.x, smem + p.offAux, wave, lane);
+      }
     }
     if constexpr (!kBf16)
       for (int i = tid; i < 2 * kMaxK * kLgS; i += kThreads) Lg[i] = 0.f;   // Lg and Mt are adjacent
@@ -450,6 +531,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
     const int Cb = p.cand_off ? (p.cand_off[b + 1] - cbase) : p.C;
     const T* __restrict__ cand = static_cast<const T*>(p.cand) + (DBG(2) ? (size_t)0 : (size_t)cbase * d);
     const int bnext = b + gridDim.x;
+    bool prefetched = false;   // next impression's history DMA already issued
+    const char* cimg = nullptr;   // candidate rows staged in the history image (bf16)
 
     if constexpr (MODE == kFull) {
       const T* __restrict__ E = static_cast<const T*>(p.hist) + (size_t)b * L * d;
@@ -457,7 +540,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
       float* S = reinterpret_cast<float*>(smem + p.offS);  // Sᵀ[k][l], [32][kMaxL] (aliases mui)
       T* Aw = reinterpret_cast<T*>(smem + p.offAw);        // A[k][l], [32][AwS]
 
-      __syncthreads();  // history DMA landed (the barrier waits vmcnt(0)); last impression's LDS reads done
+      if constexpr (kDma) vm_wait_all();   // this impression's history / mask / bias DMA landed
+      __syncthreads();                      // ... for every wave; last impression's LDS reads done
       STAMP(0);
 
       // ---- S1: Pᵀ = tanh(W1[ct] · Eᵀ) -> P[l][c] in LDS -------------------------------------
@@ -466,7 +550,12 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         if (wave < nct) {
           f32x16 acc0 = zero16(), acc1 = zero16();
           const T* w1t = W1p + (size_t)wave * ns * 1024;   // block (tile, slab 0)
-          const int l0 = min(r, L - 1), l1 = min(32 + r, L - 1);  // rows >= L: finite, dropped in S3
+          // rows >= L: finite, dropped in S3.  bf16: lane r takes history row pi(r), so the tanh'd
+          // accumulator is directly the A operand of the fused S2 product (rows l in pi order)
+          const int lr = kBf16 ? pi_row(r) : r;
+          const int l0 = min(lr, L - 1), l1 = min(32 + lr, L - 1);
+          Frag<T> qa;   // bf16 fused S2: Q[k = r][32 wave + 16h ...]
+          if constexpr (kBf16) frag_load(qa, Qp + r * (nct * 32) + wave * 32 + 16 * h);
           Frag<T> ring[PF];
 #pragma unroll
           for (int s = 0; s < PF; ++s) frag_load_tile(ring[s], w1t + min(s, ns - 1) * 1024, lane);
@@ -508,21 +597,41 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           }
 #pragma unroll
           for (int e = 0; e < 16; ++e) { acc0[e] = act_tanh<T>(acc0[e]); acc1[e] = act_tanh<T>(acc1[e]); }
-          // register e of lane (r=l, h) is c = 32*wave + 16h + e: 16 contiguous c of row l
+          // register e of lane (r, h) is c = 32*wave + 16h + e: 16 contiguous c of history row lr
           Frag<T> pf;
-          acc_to_frag(pf, acc0);
-          frag_store(Ps + r * p.PS + wave * 32 + 16 * h, pf);
-          if (L > 32) {
-            acc_to_frag(pf, acc1);
-            frag_store(Ps + (32 + r) * p.PS + wave * 32 + 16 * h, pf);
+          if constexpr (kBf16) {
+            // fused S2 partial over this wave's 32 context dims: S_w[l][k] = Σ_c P[l][c] Q[k][c];
+            // register e of lane (h, k) is l = 16h + e (A rows in pi order) -> 4 b128 stores of row k
+            float* sp = reinterpret_cast<float*>(smem + p.offS) + wave * kSPTile + r * kSPS + 16 * h;
+            f32x16 sacc = zero16();
+            acc_to_frag(pf, acc0);
+            mma_slab<T>(sacc, pf, qa);
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              reinterpret_cast<float4*>(sp)[g] = float4{sacc[4 * g], sacc[4 * g + 1], sacc[4 * g + 2], sacc[4 * g + 3]};
+            if (L > 32) {
+              sacc = zero16();
+              acc_to_frag(pf, acc1);
+              mma_slab<T>(sacc, pf, qa);
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
+                reinterpret_cast<float4*>(sp + 32)[g] = float4{sacc[4 * g], sacc[4 * g + 1], sacc[4 * g + 2], sacc[4 * g + 3]};
+            }
+          } else {
+            acc_to_frag(pf, acc0);
+            frag_store(Ps + r * p.PS + wave * 32 + 16 * h, pf);
+            if (L > 32) {
+              acc_to_frag(pf, acc1);
+              frag_store(Ps + (32 + r) * p.PS + wave * 32 + 16 * h, pf);
+            }
           }
         }
       }
       __syncthreads();
       STAMP(1);
 
-      // ---- S2: Sᵀ[k][l] = Σ_c Q[k][c] P[l][c]  (one wave per 32-position tile) ------------------
-      {
+      // ---- S2 (fp32; fused into S1 for bf16): Sᵀ[k][l] = Σ_c Q[k][c] P[l][c] ------------------
+      if constexpr (!kBf16) {
         FRESH_LANE_IDS();
         if (wave * 32 < L) {
           f32x16 acc = zero16();
@@ -538,11 +647,45 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           for (int e = 0; e < 16; ++e) S[acc_row(e, h) * kMaxL + wave * 32 + r] = acc[e];
         }
       }
-      __syncthreads();
+      if constexpr (!kBf16) __syncthreads();
       STAMP(2);
 
-      // ---- S3: masked softmax over the history (4 interests per wave, interleaved) ------------
-      {
+      // ---- S3: masked softmax over the history ----------------------------------------------
+      if constexpr (kBf16) {
+        // 16 lanes (a DPP row) per interest k = 4 wave + row, 4 positions l = 4j..4j+3 per lane;
+        // S = Σ of the nct per-wave partials of S1
+        FRESH_LANE_IDS();
+        const int k = 4 * wave + (lane >> 4), j = lane & 15;
+        const float* sp = reinterpret_cast<const float*>(smem + p.offS) + k * kSPS + 4 * j;
+        float4 sv = *reinterpret_cast<const float4*>(sp);
+        for (int w = 1; w < nct; ++w) {
+          const float4 t = *reinterpret_cast<const float4*>(sp + w * kSPTile);
+          sv = float4{sv.x + t.x, sv.y + t.y, sv.z + t.z, sv.w + t.w};
+        }
+        float v[4] = {sv.x, sv.y, sv.z, sv.w};
+        float mx = -INFINITY;
+        const char* aux = smem + p.offAux;
+        const int shift = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)b * L) & 3);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int l = 4 * j + t;
+          const bool in = l < L;
+          const bool real = in && aux[shift + l] != 0;
+          const float bl = (p.bias && in) ? reinterpret_cast<const float*>(aux + 256)[l] : 0.f;
+          v[t] = in ? (real ? v[t] + bl : 1e-30f) : -INFINITY;   // model.py:180
+          mx = fmaxf(mx, v[t]);
+        }
+        mx = row16_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          v[t] = (4 * j + t < L) ? act_exp<T>(v[t] - mx) : 0.f;
+          sum += v[t];
+        }
+        sum = row16_sum(sum);
+        const float inv = (k < K) ? 1.0f / sum : 0.f;
+        *reinterpret_cast<uint2*>(Aw + k * AwS + 4 * j) = uint2{pack_bf16x2(v[0] * inv, v[1] * inv), pack_bf16x2(v[2] * inv, v[3] * inv)};
+      } else {
         FRESH_LANE_IDS();
         const int l = lane;
         const bool in = l < L;
@@ -593,7 +736,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
               if constexpr (kBf16) {
                 // Eᵀ fragment via ds_read_b64_tr_b16: lane group g = lane>>4 reads 4 rows x 16 cols
                 const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-                const int col = i0 + 16 * (g & 1) + 4 * pp;
+                // output lane j of group g receives column i0 + pi(16(g&1) + j) (A rows in pi order)
+                const int col = i0 + 16 * (pp & 1) + 8 * (g & 1) + 4 * (pp >> 1);
                 const int ch = col >> 3, sub8 = (col & 7) * 2;
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
@@ -613,18 +757,39 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
                   bf.q[e >> 2][e & 3] = __float_as_uint(E[(size_t)l * d + i0 + r]);
                 }
               }
-              mma_slab<T>(acc, ls == 0 ? af0 : af1, bf);
+              if constexpr (kBf16) mma_slab<T>(acc, bf, ls == 0 ? af0 : af1);   // muiᵀ = Eᵀ·Aᵀ
+              else mma_slab<T>(acc, ls == 0 ? af0 : af1, bf);
             }
           }
+          if constexpr (kBf16) {
+            // register e of lane (h, k) is muiᵀ[i0 + 16h + e][k]: 16 contiguous elements of row k
+            Frag<T> mf;
+            acc_to_frag(mf, acc);
+            frag_store(muiL + r * msE + i0 + 16 * h, mf);
+            if (p.mui_out && r < K) {
+              float4* o = reinterpret_cast<float4*>(p.mui_out + ((size_t)b * K + r) * d + i0 + 16 * h);
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int k = acc_row(e, h);
-            muiL[k * msE + i0 + r] = from_f32<T>(acc[e]);
-            if (p.mui_out && k < K) p.mui_out[((size_t)b * K + k) * d + i0 + r] = acc[e];
+              for (int g = 0; g < 4; ++g) o[g] = float4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int k = acc_row(e, h);
+              muiL[k * msE + i0 + r] = from_f32<T>(acc[e]);
+              if (p.mui_out && k < K) p.mui_out[((size_t)b * K + k) * d + i0 + r] = acc[e];
+            }
           }
         }
       }
       __syncthreads();  // history region free from here on
+      if constexpr (kDma) {
+        // this impression's candidate rows -> the history image, landing during S5
+        if (need_scores && Cb > 0 && Cb <= kCChunk && ((Cb * rowB + 1023) & ~1023) <= p.eimg) {
+          FRESH_LANE_IDS();
+          dma_rows(cand, Cb, d, ldsE, wave, lane);
+          cimg = ldsE;
+        }
+      }
       STAMP(4);
     } else {  // MODE == kTaa: multi_user_interest comes from global (query)
       FRESH_LANE_IDS();
@@ -652,6 +817,15 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           else if (nm == 1) s5_gelu<T, PF, 1>(xf, W2p, muiL, msE, d, wave, lane);
         }
       }
+      Frag<T> am[kMaxJ];   // bf16 full: the wave's mui fragments, held across the candidate chunks
+      if constexpr (kDma) {
+        FRESH_LANE_IDS();
+        const int nm = (ns - wave + kWaves - 1) / kWaves;
+#pragma unroll
+        for (int m = 0; m < kMaxJ; ++m)
+          if (m < nm) frag_load(am[m], muiL + r * msE + (wave + kWaves * m) * 32 + 16 * h);
+      }
+      if (cimg) { vm_wait_all(); __syncthreads(); }   // candidate rows landed for every wave
       STAMP_SYNC();
       STAMP(5);
 
@@ -662,10 +836,19 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           const int nm = (ns - wave + kWaves - 1) / kWaves;
           f32x16 lg[2], mt[2];
           lg[0] = lg[1] = mt[0] = mt[1] = zero16();
-          if (weighted) s6_dispatch<T, true, MODE == kFull>(nm, lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
-          else s6_dispatch<T, false, MODE == kFull>(nm, lg, mt, xf, cand, Cb, cc, d, wave, r, h, muiL, msE);
+          if (weighted) s6_dispatch<T, true, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
+          else s6_dispatch<T, false, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
           STAMP_SYNC();
           STAMP(6);
+          if constexpr (kDma) {
+            // the partial slabs overwrite mui; every wave is done with mui and the candidate image
+            __syncthreads();
+            if (cimg && bnext < p.B && !DBG(4)) {   // single chunk: next impression's history now
+              dma_rows(static_cast<const T*>(p.hist) + (size_t)bnext * L * d, L, d, ldsE, wave, lane);
+              dma_aux(p.mask, p.bias, p.B, L, bnext, smem + p.offAux, wave, lane);
+              prefetched = true;
+            }
+          }
           if constexpr (kBf16) {
             // two-round reduction through LDS with plain stores: waves 0-3 store, 4-7 add
             float* slot = part + (wave & 3) * kPartWave;
@@ -787,8 +970,10 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
 
     if constexpr (kDma) {
       FRESH_LANE_IDS();
-      if (bnext < p.B && !DBG(4))   // the history region (and the partial slabs aliasing it) is free now
-        dma_history(static_cast<const T*>(p.hist) + (size_t)bnext * L * d, L, d, ldsE, wave, lane);
+      if (!prefetched && bnext < p.B && !DBG(4)) {   // the history region is free now
+        dma_rows(static_cast<const T*>(p.hist) + (size_t)bnext * L * d, L, d, ldsE, wave, lane);
+        dma_aux(p.mask, p.bias, p.B, L, bnext, smem + p.offAux, wave, lane);
+      }
     }
     STAMP(9);
   }
@@ -844,7 +1029,7 @@ __global__ void pack_weights_kernel(const T* __restrict__ W1, const T* __restric
 inline int round16(int x) { return (x + 15) & ~15; }
 
 struct Carve {
-  int MS, PS, offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, total;
+  int MS, PS, offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux, eimg, total;
 };
 
 // LDS carve (bytes).
@@ -862,17 +1047,20 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   c.PS = n_ctiles(Dc) * 32 + (bf ? 8 : 4);
   const int pbytes = round16(64 * c.PS * es);
   const int r2a = 32 * c.MS;
-  const int r2b = pbytes + kMaxK * kMaxL * 4;
+  int r2b = bf ? n_ctiles(Dc) * kSPTile * 4 : pbytes + kMaxK * kMaxL * 4;
+  if (bf && parts > r2b) r2b = parts;      // bf16 full: the S6 partial slabs live here too
   const int r2 = round16(mode == kFull ? (r2a > r2b ? r2a : r2b) : r2a);
   const int aw = mode == kFull ? (bf ? 32 * 72 * 2 : 32 * 68 * 4) : 0;
   int off = 0;
   if (bf) {
     const int eimg = mode == kFull ? (L * d * 2 + 1023) & ~1023 : 0;   // whole 1 KiB DMA blocks
     c.offE = 0;
-    c.offPart = 0;
-    const int r1 = eimg > parts ? eimg : parts;
+    c.eimg = eimg;
+    c.offPart = 0;                                  // TAA: [partial slabs | mui]
+    const int r1 = mode == kFull ? eimg : parts;
     c.offZ = round16(r1);
-    off = c.offZ + (mode == kFull ? 64 : 0);
+    c.offAux = c.offZ + 64;                         // mask words (256 B) + bias (256 B)
+    off = mode == kFull ? c.offAux + 512 : c.offZ;
     c.offLg = c.offMt = 0;
   } else {
     c.offE = c.offZ = c.offPart = 0;
@@ -882,7 +1070,8 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   }
   c.offMui = round16(off);
   c.offP = c.offMui;                       // P lives in the mui region until S4 overwrites it
-  c.offS = c.offMui + pbytes;              // S too
+  c.offS = bf ? c.offMui : c.offMui + pbytes;   // S too (bf16: the per-wave S partials of S1)
+  if (bf && mode == kFull) c.offPart = c.offMui;   // full: after S6 products mui is dead
   c.offAw = round16(c.offMui + r2);
   c.total = c.offAw + aw;
   return c;
@@ -932,6 +1121,7 @@ int run(void* stream, int dtype, int mode, Params prm) {
   const Carve c = carve(dtype, mode, prm.L, prm.d, prm.Dc);
   prm.MS = c.MS; prm.PS = c.PS; prm.offE = c.offE; prm.offZ = c.offZ; prm.offP = c.offP; prm.offS = c.offS;
   prm.offMui = c.offMui; prm.offAw = c.offAw; prm.offPart = c.offPart; prm.offLg = c.offLg; prm.offMt = c.offMt;
+  prm.offAux = c.offAux; prm.eimg = c.eimg;
   if (dtype == MINER_DTYPE_BF16) {
     // bf16 kernels specialised on the embedding dim (d = 32*NS) so the slab loops fully unroll
     switch (prm.d) {
