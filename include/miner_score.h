@@ -20,8 +20,7 @@
  *
  * Conventions (all entry points):
  *   - every pointer is caller-owned DEVICE memory, row-major and contiguous, 16-byte aligned;
- *     nothing is allocated inside (scratch is the caller's `workspace`), nothing synchronises:
- *     work is enqueued on `stream`
+ *     nothing is allocated inside, nothing synchronises: work is enqueued on `stream`
  *     (a hipStream_t; NULL = the default stream) and the call returns immediately;
  *   - `dtype` selects the element type of the activation AND weight tensors
  *     (MINER_DTYPE_F32 = exact fp32 arithmetic, the parity mode; MINER_DTYPE_BF16 = bf16 operands
@@ -41,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MINER_ABI_VERSION 3
+#define MINER_ABI_VERSION 2
 
 enum miner_dtype { MINER_DTYPE_F32 = 0, MINER_DTYPE_BF16 = 1 };
 
@@ -89,21 +88,12 @@ int miner_pack_weights(void* stream, int dtype, const void* w_poly, const void* 
  *   scores       [sum C_b]  fp32   matching scores (model.py:138 second output); may be NULL
  *                                  only when score_type == NONE
  *   user_out     [B, K, d]  fp32   optional multi_user_interest (model.py:138 first output)
- *   workspace               -      optional caller-owned device scratch of
- *                                  miner_score_workspace_bytes() bytes (16-byte aligned). With it,
- *                                  bf16 scoring runs the impression-pair kernel (one W2 stream
- *                                  per two impressions); NULL (or too small) = the single-
- *                                  impression kernel, same results. It must not be shared by
- *                                  calls that can run concurrently (other streams).
  */
 int miner_score(void* stream, int dtype, int score_type,
                 const void* history, const uint8_t* his_mask, const float* his_bias,
                 const void* candidates, const int32_t* cand_offsets, const void* packed_weights,
                 int B, int L, int C, int d, int Dc, int K,
-                float* scores, float* user_out, void* workspace, size_t workspace_bytes);
-
-/* Bytes of the miner_score workspace for this shape on the current device (0 = none used). */
-size_t miner_score_workspace_bytes(int dtype, int score_type, int L, int d, int Dc, int K);
+                float* scores, float* user_out);
 
 /*
  * TargetAwareAttention.forward (model.py:200-216) on its own:

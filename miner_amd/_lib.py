@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MINER_HIP_LIB", os.path.join(_HERE, "libminer_hip.so"
 DTYPE_F32, DTYPE_BF16 = 0, 1
 SCORE_WEIGHTED, SCORE_MAX, SCORE_MEAN, SCORE_NONE = 0, 1, 2, 3
 SCORE_TYPES = {"weighted": SCORE_WEIGHTED, "max": SCORE_MAX, "mean": SCORE_MEAN, "none": SCORE_NONE}
-ABI_VERSION = 3
+ABI_VERSION = 2
 
 # every symbol include/miner_score.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
@@ -24,8 +24,7 @@ _I = ctypes.c_int
 SIGNATURES = {
     "miner_packed_weights_bytes": (ctypes.c_size_t, [_I, _I, _I, _I]),
     "miner_pack_weights": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _P]),
-    "miner_score": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, ctypes.c_size_t]),
-    "miner_score_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
+    "miner_score": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "miner_target_aware": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "miner_supported": (_I, [_I, _I, _I, _I, _I]),
     "miner_lds_bytes": (_I, [_I, _I, _I, _I, _I]),

@@ -75,10 +75,7 @@ constexpr int kSPTile = kMaxK * kSPS;  // one wave's S partial (floats)
 enum Mode { kFull = 0, kTaa = 1 };
 
 #ifndef MINER_PF_S1
-#define MINER_PF_S1 6      // register prefetch depth of the W1 ring (S1)
-#endif
-#ifndef MINER_PF_PAIR
-#define MINER_PF_PAIR 3    // register prefetch depth of the pair kernel's weight rings
+#define MINER_PF_S1 3      // register prefetch depth of the W1 ring (S1; 6 and 8 measured slower)
 #endif
 
 struct Params {
@@ -97,8 +94,6 @@ struct Params {
   int PS;       // P row stride (elements)
   int offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux;
   int eimg;     // bytes of the history image (bf16): the candidate rows may be staged there
-  int region;   // pair kernel: bytes of each of the two LDS regions
-  void* ws;     // pair kernel: per-workgroup L2 scratch for the first impression's mui (bf16)
   int dbg;      // ablation bits, honoured only by the -DMINER_STAMPS diagnostic build
 };
 
@@ -324,31 +319,9 @@ __device__ __forceinline__ void dma_b32(const void* g, unsigned lds) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
                : "=&s"(t) : "v"(g), "s"(lds) : "memory");
 }
-// agent-scope (sc1) variant: misses the CU's vector L1, for lines this CU itself stored earlier
-__device__ __forceinline__ void dma_b128_l2(const void* g, unsigned lds) {
-  unsigned t;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
-               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
-}
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// wait until at most n (wave-uniform, clamped to 15) vector-memory operations are outstanding
-__device__ __forceinline__ void vm_wait_le(int n) {
-  switch (n < 15 ? n : 15) {
-#define MINER_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    MINER_VMW(0) MINER_VMW(1) MINER_VMW(2) MINER_VMW(3) MINER_VMW(4) MINER_VMW(5) MINER_VMW(6) MINER_VMW(7)
-    MINER_VMW(8) MINER_VMW(9) MINER_VMW(10) MINER_VMW(11) MINER_VMW(12) MINER_VMW(13) MINER_VMW(14)
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-#undef MINER_VMW
-  }
-}
-// number of 1 KiB blocks dma_rows(nrows rows of d) issues from `wave`
-__device__ __forceinline__ int dma_rows_blocks(int nrows, int d, int wave) {
-  const int nblk = (nrows * (d >> 3) + 63) >> 6;
-  return wave < nblk ? (nblk - wave + kWaves - 1) / kWaves : 0;
-}
-
 // nrows rows of d elements -> the swizzled image (whole 1 KiB blocks, one per wave-instruction)
-template <class T, bool L2ONLY = false>
+template <class T>
 __device__ __forceinline__ void dma_rows(const T* src, int nrows, int d, char* img, int wave, int lane) {
   const int cpr = d >> 3;                 // 16-byte chunks per row
   const int g16 = (cpr & 15) == 0;
@@ -359,33 +332,9 @@ __device__ __forceinline__ void dma_rows(const T* src, int nrows, int d, char* i
     const int row = pos / cpr;
     const int c = pos - row * cpr;
     const T* g = (pos < total) ? src + (size_t)row * d + (size_t)((c ^ eswz(row, g16)) << 3) : src;
-    if (L2ONLY) dma_b128_l2(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
-    else dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
+    dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
   }
 }
-
-// dma_rows split into steps, so the wave can interleave the (TA-rate-bound, 16 clk per 1 KiB block
-// per CU) DMA instructions with VALU work instead of stalling behind them
-template <class T>
-struct DmaRows {
-  const T* src;
-  char* img;
-  int d, total, nblk, blk, lane;
-  __device__ __forceinline__ DmaRows(const T* s, int nrows, int d_, char* im, int wave, int ln)
-      : src(s), img(im), d(d_), total(nrows * (d_ >> 3)), nblk((nrows * (d_ >> 3) + 63) >> 6), blk(wave), lane(ln) {}
-  __device__ __forceinline__ void step(int n) {
-    const int cpr = d >> 3;
-    const int g16 = (cpr & 15) == 0;
-    for (int i = 0; i < n && blk < nblk; ++i, blk += kWaves) {
-      const int pos = blk * 64 + lane;
-      const int row = pos / cpr;
-      const int c = pos - row * cpr;
-      const T* g = (pos < total) ? src + (size_t)row * d + (size_t)((c ^ eswz(row, g16)) << 3) : src;
-      dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
-    }
-  }
-  __device__ __forceinline__ void rest() { step(1 << 20); }
-};
 
 // impression b's mask bytes (as the aligned words covering them) and fp32 bias -> the aux block
 __device__ __forceinline__ void dma_aux(const uint8_t* mask, const float* bias, int B, int L, int b, char* aux,
@@ -954,7 +903,9 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
       }
       __syncthreads();  // history region free from here on
       if constexpr (kDma) {
-        // this impression's candidate rows -> the history image, landing during S5
+        // This impression's candidate rows -> the (dead) history image, landing during S5.  Issued
+        // before S5's ring: an untracked DMA issued inside the ring, older than later ring loads,
+        // would make each of their waits cover its HBM latency too (measured: S5 +6K cycles).
         if (need_scores && Cb > 0 && Cb <= kCChunk && ((Cb * rowB + 1023) & ~1023) <= p.eimg) {
           FRESH_LANE_IDS();
           dma_rows(cand, Cb, d, ldsE, wave, lane);
@@ -1086,502 +1037,6 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   STAMP_FLUSH(n_done);
 }
 
-// =============================================================================================
-// bf16 impression-pair kernel: one W2 stream (S5) serves two impressions
-// =============================================================================================
-// LDS holds two regions of equal size (each >= the history image, the S partials, a mui image,
-// the S6 partial slabs) plus the zero block, the mask/bias aux block and Aw.  For the pair
-// (b0, b1), with E(b0) already in region X:
-//   S1(b0) X -> S partials in Y;  S3(b0) -> Aw;  DMA E(b1), aux(b1) -> Y (hidden behind S4(b0));
-//   S4(b0) -> mui(b0) rows to the workgroup's L2 scratch (+ mui_out);
-//   S1(b1) Y -> partials in X;  S3(b1);  S4(b1) -> mui(b1) image in X (+ mui_out);
-//   DMA mui(b0) scratch -> Y image;  S5: W2 streamed once, B operands from both images;
-//   mui fragments -> registers;  DMA cand(b0) -> Y, cand(b1) -> X;  GELU;
-//   S6/S7(b0) in Y;  DMA E(next b0), aux -> Y;  S6/S7(b1) in X;  then X and Y swap roles.
-// The S5 weight bytes per impression halve (the stage is bound by the L2 -> CU stream).
-
-// per-workgroup scratch: mui(b0) rows [32][d], mui(b1) rows [32][d], parked X(b1) fragments
-__host__ __device__ inline int pair_ws_slot_bytes(int d) { return (64 * d + kWaves * kMaxJ * 2 * 64 * 8) * 2; }
-
-// S1 (+ fused S2) of one impression: history image `img` -> per-wave S partials `spo`
-template <int NS>
-__device__ __forceinline__ void pair_s1(const char* img, float* spo, const __bf16* __restrict__ W1p,
-                                        const __bf16* __restrict__ Qp, int L, int nct) {
-  using T = __bf16;
-  constexpr int PF = MINER_PF_S1, ns = NS, d = 32 * NS, rowB = 2 * d;
-  constexpr int g16 = ((d >> 3) & 15) == 0;
-  FRESH_LANE_IDS();
-  if (wave >= nct) return;
-  f32x16 acc0 = zero16(), acc1 = zero16();
-  const T* w1t = W1p + (size_t)wave * ns * 1024;
-  const int lr = pi_row(r);
-  const int l0 = min(lr, L - 1), l1 = min(32 + lr, L - 1);
-  Frag<T> qa;
-  frag_load(qa, Qp + r * (nct * 32) + wave * 32 + 16 * h);
-  Frag<T> ring[PF];
-#pragma unroll
-  for (int s = 0; s < PF; ++s) frag_load_tile(ring[s], w1t + min(s, ns - 1) * 1024, lane);
-  int j = 0;
-#pragma unroll
-  for (; j + PF <= ns; j += PF) {
-#pragma unroll
-    for (int s = 0; s < PF; ++s) {
-      Frag<T> b0, b1;
-      frag_load_E(b0, img, l0, (j + s) * 32, h, rowB, g16);
-      frag_load_E(b1, img, l1, (j + s) * 32, h, rowB, g16);
-      mma_slab<T>(acc0, ring[s], b0);
-      mma_slab<T>(acc1, ring[s], b1);
-      frag_load_tile(ring[s], w1t + min(j + s + PF, ns - 1) * 1024, lane);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < PF; ++s) {
-    if (j + s < ns) {
-      Frag<T> b0, b1;
-      frag_load_E(b0, img, l0, (j + s) * 32, h, rowB, g16);
-      frag_load_E(b1, img, l1, (j + s) * 32, h, rowB, g16);
-      mma_slab<T>(acc0, ring[s], b0);
-      mma_slab<T>(acc1, ring[s], b1);
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 16; ++e) { acc0[e] = tanh_fast(acc0[e]); acc1[e] = tanh_fast(acc1[e]); }
-  float* sp = spo + wave * kSPTile + r * kSPS + 16 * h;
-  Frag<T> pf;
-  f32x16 sacc = zero16();
-  acc_to_frag(pf, acc0);
-  mma_slab<T>(sacc, pf, qa);
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-    reinterpret_cast<float4*>(sp)[g] = float4{sacc[4 * g], sacc[4 * g + 1], sacc[4 * g + 2], sacc[4 * g + 3]};
-  if (L > 32) {
-    sacc = zero16();
-    acc_to_frag(pf, acc1);
-    mma_slab<T>(sacc, pf, qa);
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      reinterpret_cast<float4*>(sp + 32)[g] = float4{sacc[4 * g], sacc[4 * g + 1], sacc[4 * g + 2], sacc[4 * g + 3]};
-  }
-}
-
-// S3 of one impression: Σ of the nct S partials, mask fill 1e-30, softmax over L -> Aw (bf16)
-__device__ __forceinline__ void pair_s3(const float* spi, int nct, const char* aux, int shift, bool has_bias, int L,
-                                        int K, __bf16* Aw) {
-  FRESH_LANE_IDS();
-  const int k = 4 * wave + (lane >> 4), j = lane & 15;
-  const float* sp = spi + k * kSPS + 4 * j;
-  float4 sv = *reinterpret_cast<const float4*>(sp);
-  for (int w = 1; w < nct; ++w) {
-    const float4 t = *reinterpret_cast<const float4*>(sp + w * kSPTile);
-    sv = float4{sv.x + t.x, sv.y + t.y, sv.z + t.z, sv.w + t.w};
-  }
-  float v[4] = {sv.x, sv.y, sv.z, sv.w};
-  float mx = -INFINITY;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int l = 4 * j + t;
-    const bool in = l < L;
-    const bool real = in && aux[shift + l] != 0;
-    const float bl = (has_bias && in) ? reinterpret_cast<const float*>(aux + 256)[l] : 0.f;
-    v[t] = in ? (real ? v[t] + bl : 1e-30f) : -INFINITY;   // model.py:180
-    mx = fmaxf(mx, v[t]);
-  }
-  mx = row16_max(mx);
-  float sum = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    v[t] = (4 * j + t < L) ? __expf(v[t] - mx) : 0.f;
-    sum += v[t];
-  }
-  sum = row16_sum(sum);
-  const float inv = (k < K) ? 1.0f / sum : 0.f;
-  *reinterpret_cast<uint2*>(Aw + k * 72 + 4 * j) = uint2{pack_bf16x2(v[0] * inv, v[1] * inv), pack_bf16x2(v[2] * inv, v[3] * inv)};
-}
-
-// S4 of one impression: muiᵀ tiles of the wave's d-tiles (register e of lane (h, k) is
-// muiᵀ[32 it + 16h + e][k]) from the history image at LDS offset imgOff and Aw
-template <int NS>
-__device__ __forceinline__ void pair_s4(const char* smem, int imgOff, int zOff, const __bf16* Aw, int L,
-                                        f32x16 (&acc)[kMaxJ]) {
-  constexpr int NM = NS / kWaves;
-  using T = __bf16;
-  constexpr int ns = NS, d = 32 * NS, rowB = 2 * d;
-  constexpr int g16 = ((d >> 3) & 15) == 0;
-  FRESH_LANE_IDS();
-  const int nLs = (L + 31) >> 5;
-  Frag<T> af0, af1;
-  frag_load(af0, Aw + r * 72 + 16 * h);
-  if (nLs > 1) frag_load(af1, Aw + r * 72 + 32 + 16 * h); else frag_zero(af1);
-  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-#pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    const int it = wave + kWaves * m;
-    {
-      const int i0 = it * 32;
-      acc[m] = zero16();
-#pragma unroll
-      for (int ls = 0; ls < 2; ++ls) {
-        if (ls < nLs) {
-          Frag<T> bf;
-          const int lb = ls * 32;
-          const int col = i0 + 16 * (pp & 1) + 8 * (g & 1) + 4 * (pp >> 1);
-          const int ch = col >> 3, sub8 = (col & 7) * 2;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const int row = lb + 16 * (g >> 1) + 8 * s + 4 * u + q;
-              const int off = (row < L) ? (imgOff + row * rowB + ((ch ^ eswz(row, g16)) << 4) + sub8) : zOff;
-              const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)((lds_char*)smem + off));
-              bf.q[s][2 * u] = (unsigned)(unsigned short)v[0] | ((unsigned)(unsigned short)v[1] << 16);
-              bf.q[s][2 * u + 1] = (unsigned)(unsigned short)v[2] | ((unsigned)(unsigned short)v[3] << 16);
-            }
-          }
-          mma_slab<T>(acc[m], bf, ls == 0 ? af0 : af1);
-        }
-      }
-    }
-  }
-}
-
-// S5 for the pair: raw (pre-GELU) accumulators of X0 = W2·mui0ᵀ and X1 = W2·mui1ᵀ over the
-// wave's NM d-tiles; the B operands come from the two mui images.  The caller has issued the
-// DMA of img0: the ring prologue goes out first, then every wave waits for all of it.
-template <int PF, int NM, int NS>
-__device__ __forceinline__ void pair_s5(f32x16 (&acc0)[kMaxJ], f32x16 (&acc1)[kMaxJ], const __bf16* __restrict__ W2p,
-                                        const char* img0, const char* img1) {
-  using T = __bf16;
-  constexpr int ns = NS, d = 32 * NS, rowB = 2 * d;
-  constexpr int g16 = ((d >> 3) & 15) == 0;
-  FRESH_LANE_IDS();
-  const T* w2t[NM];
-#pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    acc0[m] = zero16();
-    acc1[m] = zero16();
-    w2t[m] = W2p + (size_t)(wave + kWaves * m) * ns * 1024;
-  }
-  Frag<T> ring[PF][NM];
-#pragma unroll
-  for (int s = 0; s < PF; ++s)
-#pragma unroll
-    for (int m = 0; m < NM; ++m) frag_load_tile(ring[s][m], w2t[m] + min(s, ns - 1) * 1024, lane);
-  vm_wait_all();
-  __syncthreads();   // img0 (DMA'd mui of the first impression) landed for every wave
-  int j = 0;
-#pragma unroll
-  for (; j + PF <= ns; j += PF) {
-#pragma unroll
-    for (int s = 0; s < PF; ++s) {
-      Frag<T> bm0, bm1;
-      frag_load_E(bm0, img0, r, (j + s) * 32, h, rowB, g16);
-      frag_load_E(bm1, img1, r, (j + s) * 32, h, rowB, g16);
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        mma_slab<T>(acc0[m], ring[s][m], bm0);
-        mma_slab<T>(acc1[m], ring[s][m], bm1);
-      }
-#pragma unroll
-      for (int m = 0; m < NM; ++m) frag_load_tile(ring[s][m], w2t[m] + min(j + s + PF, ns - 1) * 1024, lane);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < PF; ++s) {
-    if (j + s < ns) {
-      Frag<T> bm0, bm1;
-      frag_load_E(bm0, img0, r, (j + s) * 32, h, rowB, g16);
-      frag_load_E(bm1, img1, r, (j + s) * 32, h, rowB, g16);
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        mma_slab<T>(acc0[m], ring[s][m], bm0);
-        mma_slab<T>(acc1[m], ring[s][m], bm1);
-      }
-    }
-  }
-}
-
-// One candidate chunk [cc, cc+64) of one impression: S6 products, reduction into `part`, S7.
-// `pre` runs right after the products barrier (the partial region is free from then on).
-template <int NM, class F>
-__device__ __forceinline__ void pair_chunk(const Params& p, int cbase, int Cb, int cc, bool write,
-                                           const Frag<__bf16> (&xf)[kMaxJ], const Frag<__bf16> (&am)[kMaxJ],
-                                           const __bf16* cand, const char* cimg, float* part, int d, F&& pre) {
-  using T = __bf16;
-  {
-    FRESH_LANE_IDS();
-    f32x16 lg[2], mt[2];
-    if (p.score_type == MINER_SCORE_WEIGHTED)
-      s6_products<T, NM, true, true>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, nullptr, 0);
-    else
-      s6_products<T, NM, false, true>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, nullptr, 0);
-    __syncthreads();   // the candidate image (the partials' region) is read
-    pre();
-    s6_reduce_bf16(part, lg, mt, wave, r, h, false);
-  }
-  __syncthreads();
-  {
-    FRESH_LANE_IDS();
-    const int cl = tid >> 3, sub = tid & 7;
-    const int c = cc + cl;
-    float lgv[4], mtv[4];
-    s7_load_bf16(part, cl, sub, lgv, mtv);
-    bool kv[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) kv[jj] = 4 * sub + jj < p.K;
-    const float sc = s7_score<T>(lgv, mtv, kv, p.score_type, p.K);
-    if (write && sub == 0 && c < Cb) p.scores[cbase + c] = sc;
-  }
-  __syncthreads();
-}
-
-// S6 + S7 of one impression.  `pre` runs once, after the LAST chunk's products (it defines
-// registers live after this call: inside the chunk loop they would be live around its back-edge).
-template <int NM, class F>
-__device__ __forceinline__ void pair_score(const Params& p, int b, bool write, const Frag<__bf16> (&xf)[kMaxJ],
-                                           const Frag<__bf16> (&am)[kMaxJ], const char* cimg, float* part, int d,
-                                           F&& pre) {
-  using T = __bf16;
-  const int cbase = p.cand_off ? p.cand_off[b] : b * p.C;
-  const int Cb = p.cand_off ? (p.cand_off[b + 1] - cbase) : p.C;
-  const T* __restrict__ cand = static_cast<const T*>(p.cand) + (size_t)cbase * d;
-  if (Cb <= 0) { pre(); return; }
-  int cc = 0;
-  for (; cc + kCChunk < Cb; cc += kCChunk)
-    pair_chunk<NM>(p, cbase, Cb, cc, write, xf, am, cand, cimg, part, d, [] {});
-  pair_chunk<NM>(p, cbase, Cb, cc, write, xf, am, cand, cimg, part, d, pre);
-}
-
-template <int NS>
-__global__ __launch_bounds__(kThreads) void miner_pair(Params p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  using T = __bf16;
-  static_assert(NS % kWaves == 0, "pair kernel: every wave owns NS/8 d-tiles");
-  constexpr int PF = MINER_PF_PAIR, ns = NS, d = 32 * NS, rowB = 2 * d, NM = NS / kWaves;
-  constexpr int g16 = ((d >> 3) & 15) == 0;
-  (void)ns;
-  const int L = p.L, K = p.K, nct = n_ctiles(p.Dc);
-  const T* __restrict__ W1p = static_cast<const T*>(p.wp);
-  const T* __restrict__ Qp = W1p + w1p_elems(d, p.Dc);
-  const T* __restrict__ W2p = Qp + qp_elems(p.Dc);
-  const T* __restrict__ hist = static_cast<const T*>(p.hist);
-  char* aux = smem + p.offAux;
-  T* Aw = reinterpret_cast<T*>(smem + p.offAw);
-  T* scratch = reinterpret_cast<T*>(static_cast<char*>(p.ws) + (size_t)blockIdx.x * pair_ws_slot_bytes(d));
-  const int npairs = (p.B + 1) >> 1;
-  int offX = p.offE, offY = p.offE + p.region;
-  const bool weighted = p.score_type == MINER_SCORE_WEIGHTED;
-  auto mshift = [&](int b) { return (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)b * L) & 3); };
-  auto stageable = [&](int b) {
-    const int Cb = p.cand_off ? p.cand_off[b + 1] - p.cand_off[b] : p.C;
-    return Cb > 0 && Cb <= kCChunk && ((Cb * rowB + 1023) & ~1023) <= p.region;
-  };
-  auto cand_of = [&](int b) {
-    return static_cast<const T*>(p.cand) + (size_t)(p.cand_off ? p.cand_off[b] : b * p.C) * d;
-  };
-  auto ncand = [&](int b) { return p.cand_off ? p.cand_off[b + 1] - p.cand_off[b] : p.C; };
-  {
-    FRESH_LANE_IDS();
-    if (tid < 4) reinterpret_cast<u32x4*>(smem + p.offZ)[tid] = u32x4{0u, 0u, 0u, 0u};
-    if ((int)blockIdx.x < npairs) {
-      dma_rows(hist + (size_t)(2 * blockIdx.x) * L * d, L, d, smem + offX, wave, lane);
-      dma_aux(p.mask, p.bias, p.B, L, 2 * blockIdx.x, aux, wave, lane);
-    }
-  }
-  STAMP_DECL
-  int n_done = 0;
-  for (int q = blockIdx.x; q < npairs; q += gridDim.x) {
-    n_done += 2;
-    const int b0 = 2 * q;
-    const bool has1 = b0 + 1 < p.B;
-    const int b1 = has1 ? b0 + 1 : b0;
-    char* X = smem + offX;
-    char* Y = smem + offY;
-    f32x16 acc[kMaxJ];
-#pragma unroll
-    for (int m = 0; m < kMaxJ; ++m) acc[m] = zero16();
-
-    // ---- first impression: S1, S3 ----------------------------------------------------------
-    vm_wait_all();
-    __syncthreads();                    // E(b0) and aux(b0) landed; the previous pair is done
-    STAMP(0);
-    pair_s1<NS>(X, reinterpret_cast<float*>(Y), W1p, Qp, L, nct);
-    __syncthreads();
-    STAMP(1);
-    pair_s3(reinterpret_cast<const float*>(Y), nct, aux, mshift(b0), p.bias != nullptr, L, K, Aw);
-    __syncthreads();                    // S partials and aux read: Y and aux are free
-    {
-      FRESH_LANE_IDS();
-      dma_rows(hist + (size_t)b1 * L * d, L, d, Y, wave, lane);
-      dma_aux(p.mask, p.bias, p.B, L, b1, aux, wave, lane);
-    }
-    STAMP(2);
-    // ---- first impression: S4 -> mui rows in the L2 scratch --------------------------------
-    pair_s4<NS>(smem, offX, p.offZ, Aw, L, acc);
-    {
-      FRESH_LANE_IDS();
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const int i0 = (wave + kWaves * m) * 32;
-        {
-          Frag<T> mf;
-          acc_to_frag(mf, acc[m]);
-          frag_store(scratch + r * d + i0 + 16 * h, mf);
-          if (p.mui_out && r < K) {
-            float4* o = reinterpret_cast<float4*>(p.mui_out + ((size_t)b0 * K + r) * d + i0 + 16 * h);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) o[g] = float4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
-          }
-        }
-      }
-    }
-    vm_wait_all();
-    __syncthreads();                    // E(b1) landed; X free; the scratch rows are in L2
-    STAMP(3);
-
-    // ---- second impression: S1, S3, S4 -> mui image in X -----------------------------------
-    pair_s1<NS>(Y, reinterpret_cast<float*>(X), W1p, Qp, L, nct);
-    __syncthreads();
-    STAMP(4);
-    pair_s3(reinterpret_cast<const float*>(X), nct, aux, mshift(b1), p.bias != nullptr, L, K, Aw);
-    __syncthreads();
-    pair_s4<NS>(smem, offY, p.offZ, Aw, L, acc);
-    {
-      FRESH_LANE_IDS();
-      const int sw = eswz(r, g16);
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const int i0 = (wave + kWaves * m) * 32;
-        {
-          Frag<T> mf;
-          acc_to_frag(mf, acc[m]);
-          const int c0 = (i0 + 16 * h) >> 3;
-          char* row = X + r * rowB;
-          *reinterpret_cast<u32x4*>(row + ((c0 ^ sw) << 4)) = mf.q[0];
-          *reinterpret_cast<u32x4*>(row + (((c0 + 1) ^ sw) << 4)) = mf.q[1];
-          frag_store(scratch + 32 * d + r * d + i0 + 16 * h, mf);   // rows again, for S6's reload
-          if (has1 && p.mui_out && r < K) {
-            float4* o = reinterpret_cast<float4*>(p.mui_out + ((size_t)b1 * K + r) * d + i0 + 16 * h);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) o[g] = float4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
-          }
-        }
-      }
-    }
-    __syncthreads();                    // E(b1) read: Y free; mui(b1) image complete in X
-    STAMP(5);
-    {
-      FRESH_LANE_IDS();
-      dma_rows<T, true>(scratch, 32, d, Y, wave, lane);   // mui(b0) back, as an image in Y
-    }
-
-    // ---- S5 for both -----------------------------------------------------------------------
-    f32x16 acc1[kMaxJ];
-#pragma unroll
-    for (int m = 0; m < kMaxJ; ++m) acc1[m] = zero16();
-    if (weighted) {
-      pair_s5<PF, NM, NS>(acc, acc1, W2p, Y, X);
-    } else {
-      vm_wait_all();
-      __syncthreads();
-    }
-    // Registers cannot hold both impressions' S6 operands through S6(b0): the second
-    // impression's X fragments are parked in the scratch and, with its mui fragments (the rows S4
-    // wrote there), reloaded during S6(b0)'s reduction — sc1 loads, past this CU's L1.
-    STAMP_SYNC();
-    STAMP(6);
-    Frag<T> am0[kMaxJ], am1[kMaxJ], xf0[kMaxJ], xf1[kMaxJ];
-#pragma unroll
-    for (int m = 0; m < kMaxJ; ++m) { frag_zero(am0[m]); frag_zero(am1[m]); frag_zero(xf0[m]); frag_zero(xf1[m]); }
-    {
-      // mui(b0) fragments from the Y image; X(b1) = gelu(acc1) -> bf16 fragments, parked in the
-      // scratch (registers cannot hold both impressions' S6 operands through S6(b0))
-      FRESH_LANE_IDS();
-#pragma unroll
-      for (int m = 0; m < NM; ++m) frag_load_E(am0[m], Y, r, (wave + kWaves * m) * 32, h, rowB, g16);
-      if (weighted) {
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          gelu_tile<T>(acc1[m]);
-          acc_to_frag(xf1[m], acc1[m]);
-          u32x4* park = reinterpret_cast<u32x4*>(scratch + 64 * d) + ((wave * kMaxJ + m) * 2) * 64 + lane;
-          park[0] = xf1[m].q[0];
-          park[64] = xf1[m].q[1];
-        }
-      }
-    }
-    STAMP_SYNC();
-    STAMP(10);
-    __syncthreads();                    // both mui images read: stage the candidate rows
-    const bool st0 = stageable(b0), st1 = stageable(b1);
-    {
-      FRESH_LANE_IDS();
-      // b0's rows first: waiting for them leaves b1's DMA in flight under S6/S7(b0); the DMA
-      // blocks are interleaved with the GELU tiles
-      DmaRows<T> c0(cand_of(b0), st0 ? ncand(b0) : 0, d, Y, wave, lane);
-      DmaRows<T> c1(cand_of(b1), st1 ? ncand(b1) : 0, d, X, wave, lane);
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        c0.step(3);
-        if (weighted) {
-          gelu_tile<T>(acc[m]);
-          acc_to_frag(xf0[m], acc[m]);
-        }
-      }
-      c0.rest();
-      c1.rest();
-      STAMP(11);
-      vm_wait_le(st1 ? dma_rows_blocks(ncand(b1), d, wave) : 0);
-    }
-    __syncthreads();                    // b0's candidate rows (and the parked X(b1)) landed
-    STAMP(7);
-
-    // ---- S6/S7: first impression in Y, second in X -----------------------------------------
-#ifndef MINER_ABL_NO_S6A
-#ifdef MINER_ABL_NO_RELOAD
-#pragma unroll
-    for (int m = 0; m < kMaxJ; ++m) { frag_zero(am1[m]); frag_zero(xf1[m]); }
-    pair_score<NM>(p, b0, true, xf0, am0, st0 ? Y : nullptr, reinterpret_cast<float*>(Y), d, [&] {});
-    if (false)
-#endif
-    pair_score<NM>(p, b0, true, xf0, am0, st0 ? Y : nullptr, reinterpret_cast<float*>(Y), d, [&] {
-      FRESH_LANE_IDS();
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, pair_ws_slot_bytes(d), 0x00020000);
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        {
-          const int ob = (32 * d + r * d + (wave + kWaves * m) * 32 + 16 * h) * 2;
-          am1[m].q[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ob, 0, 16));
-          am1[m].q[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ob + 16, 0, 16));
-          if (weighted) {
-            const int op = 64 * d * 2 + (((wave * kMaxJ + m) * 2) * 64 + lane) * 16;
-            xf1[m].q[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, op, 0, 16));
-            xf1[m].q[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, op + 64 * 16, 0, 16));
-          }
-        }
-      }
-    });
-#endif
-    vm_wait_all();
-    __syncthreads();                    // b1's candidate rows and the reloaded operands landed
-    STAMP(8);
-    const int qn = q + gridDim.x;
-#ifndef MINER_ABL_NO_S6B
-    pair_score<NM>(p, b1, has1, xf1, am1, st1 ? X : nullptr, reinterpret_cast<float*>(X), d, [&] {
-      if (qn < npairs) {   // Y is free: the next pair's first history goes there
-        FRESH_LANE_IDS();
-        dma_rows(hist + (size_t)(2 * qn) * L * d, L, d, Y, wave, lane);
-        dma_aux(p.mask, p.bias, p.B, L, 2 * qn, aux, wave, lane);
-      }
-    });
-#endif
-    STAMP(9);
-    const int t = offX; offX = offY; offY = t;
-  }
-  STAMP_FLUSH(n_done);
-}
-
 // ---------------------------------------------------------------------------------------------
 // weight packing
 // ---------------------------------------------------------------------------------------------
@@ -1631,7 +1086,7 @@ __global__ void pack_weights_kernel(const T* __restrict__ W1, const T* __restric
 inline int round16(int x) { return (x + 15) & ~15; }
 
 struct Carve {
-  int MS, PS, offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux, eimg, region, total;
+  int MS, PS, offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux, eimg, total;
 };
 
 // LDS carve (bytes).
@@ -1678,28 +1133,6 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   c.total = c.offAw + aw;
   return c;
 }
-
-// pair kernel: two equal regions (each >= history image, S partials, 32-row mui image, S6 partial
-// slabs), zero block, aux (mask words + bias), Aw
-Carve carve_pair(int L, int d, int Dc) {
-  Carve c{};
-  const int rowB = 2 * d;
-  int R = L * rowB;
-  if (n_ctiles(Dc) * kSPTile * 4 > R) R = n_ctiles(Dc) * kSPTile * 4;
-  if (32 * rowB > R) R = 32 * rowB;
-  if (4 * kPartWave * 4 > R) R = 4 * kPartWave * 4;
-  R = (R + 1023) & ~1023;
-  c.offE = 0;
-  c.region = R;
-  c.eimg = R;
-  c.offZ = 2 * R;
-  c.offAux = c.offZ + 64;
-  c.offAw = round16(c.offAux + 512);
-  c.total = c.offAw + 32 * 72 * 2;
-  return c;
-}
-
-bool pair_ns(int d) { return d == 32 * 8 || d == 32 * 16 || d == 32 * 24; }   // d/32 a multiple of 8
 
 int check_shape(int dtype, int mode, int L, int d, int Dc, int K) {
   if (dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) return MINER_EINVAL;
@@ -1761,37 +1194,6 @@ int run(void* stream, int dtype, int mode, Params prm) {
   return mode == kFull ? launch<float, kFull, 0>(stream, prm, c.total) : launch<float, kTaa, 0>(stream, prm, c.total);
 }
 
-size_t pair_workspace_bytes(int dtype, int score_type, int L, int d, int Dc, int K) {
-  if (dtype != MINER_DTYPE_BF16 || score_type == MINER_SCORE_NONE || !pair_ns(d)) return 0;
-  if (check_shape(dtype, kFull, L, d, Dc, K) != MINER_OK) return 0;
-  if (carve_pair(L, d, Dc).total > kLdsMax) return 0;
-  return (size_t)num_cus() * pair_ws_slot_bytes(d);
-}
-
-template <int NS>
-int launch_pair(void* stream, Params prm) {
-  const Carve c = carve_pair(prm.L, prm.d, prm.Dc);
-  prm.offE = c.offE; prm.region = c.region; prm.eimg = c.eimg; prm.offZ = c.offZ; prm.offAux = c.offAux;
-  prm.offAw = c.offAw;
-  auto kern = miner_pair<NS>;
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, c.total);
-  if (e != hipSuccess) return (int)e;
-  const int npairs = (prm.B + 1) / 2;
-  const int grid = npairs < num_cus() ? npairs : num_cus();   // <= the scratch slots
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), c.total, static_cast<hipStream_t>(stream), prm);
-  e = hipGetLastError();
-  return e == hipSuccess ? MINER_OK : (int)e;
-}
-
-int run_pair(void* stream, const Params& prm) {
-  switch (prm.d) {
-    case 32 * 8: return launch_pair<8>(stream, prm);
-    case 32 * 16: return launch_pair<16>(stream, prm);
-    case 32 * 24: return launch_pair<24>(stream, prm);
-    default: return MINER_ESHAPE;
-  }
-}
-
 size_t packed_bytes(int dtype, int d, int Dc) {
   const size_t es = dtype == MINER_DTYPE_BF16 ? 2 : 4;
   return (w1p_elems(d, Dc) + qp_elems(Dc) + w2p_elems(d)) * es;
@@ -1828,14 +1230,10 @@ int miner_pack_weights(void* stream, int dtype, const void* w_poly, const void* 
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
-size_t miner_score_workspace_bytes(int dtype, int score_type, int L, int d, int Dc, int K) {
-  return pair_workspace_bytes(dtype, score_type, L, d, Dc, K);
-}
-
 int miner_score(void* stream, int dtype, int score_type, const void* history, const uint8_t* his_mask,
                 const float* his_bias, const void* candidates, const int32_t* cand_offsets,
                 const void* packed_weights, int B, int L, int C, int d, int Dc, int K, float* scores,
-                float* user_out, void* workspace, size_t workspace_bytes) {
+                float* user_out) {
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
   if (B < 0 || C < 0) return MINER_EINVAL;
   const int sh = check_shape(dtype, kFull, L, d, Dc, K);
@@ -1850,11 +1248,6 @@ int miner_score(void* stream, int dtype, int score_type, const void* history, co
   prm.cand_off = cand_offsets; prm.wp = packed_weights; prm.value = nullptr; prm.scores = scores;
   prm.mui_out = user_out;
   prm.B = B; prm.L = L; prm.C = C; prm.d = d; prm.Dc = Dc; prm.K = K; prm.score_type = score_type;
-  const size_t ws = pair_workspace_bytes(dtype, score_type, L, d, Dc, K);
-  if (ws > 0 && workspace && workspace_bytes >= ws && aligned16(workspace)) {
-    prm.ws = workspace;
-    return run_pair(stream, prm);
-  }
   return run(stream, dtype, kFull, prm);
 }
 

@@ -48,22 +48,6 @@ def _stream(dev):
     return torch.cuda.current_stream(dev).cuda_stream
 
 
-_WS = {}
-
-
-def _workspace(device: torch.device, nbytes: int):
-    """miner_score scratch, cached per (device, stream): calls on one stream run in order, so
-    they can share it; another stream gets its own."""
-    if nbytes == 0:
-        return None
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
-    ws = _WS.get(key)
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        _WS[key] = ws
-    return ws
-
-
 def check_offsets(cand_offsets: torch.Tensor, B: int, N: int) -> None:
     """Host-side validation of CSR candidate offsets (one device->host copy)."""
     o = cand_offsets.detach().to("cpu", torch.int64)
@@ -120,15 +104,13 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
           w_poly, context_codes: torch.Tensor | None = None, w_target: torch.Tensor | None = None, *,
           score_type: str = "weighted", cand_offsets: torch.Tensor | None = None,
           his_bias: torch.Tensor | None = None, return_user: bool = False,
-          validate_offsets: bool = True, use_workspace: bool = True):
+          validate_offsets: bool = True):
     """Fused PolyAttention -> Cand·muiᵀ -> aggregation (src/model/model.py:113-138).
 
     history [B,L,d], his_mask [B,L] bool, candidates [B,C,d] (dense) or [N,d] with
     cand_offsets [B+1] int32 (ragged). ``w_poly`` is a PackedWeights, or the raw weight tensors are
     passed as (w_poly, context_codes, w_target). Activations float32 (parity) or bfloat16.
     Returns scores ([B,C] dense / [N] ragged, fp32) and, if return_user, mui [B,K,d] fp32.
-    ``use_workspace=False`` forces the single-impression kernel (the bf16 pair kernel needs a
-    scratch workspace; both give the same results).
     """
     st = _lib.SCORE_TYPES.get(score_type)
     if st is None or st == _lib.SCORE_NONE:
@@ -183,11 +165,9 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
         scores = torch.empty((candidates.shape[0],), device=history.device, dtype=torch.float32)
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32) if return_user else None
     with torch.cuda.device(history.device):
-        wsb = _lib.lib().miner_score_workspace_bytes(dt, st, L, d, Dc, K) if use_workspace else 0
-        ws = _workspace(history.device, wsb)
         rc = _lib.lib().miner_score(_stream(history.device), dt, st, _ptr(history), _ptr(mask), _ptr(his_bias),
                                     _ptr(candidates), _ptr(offs), _ptr(pw.buf), B, L, C, d, Dc, K,
-                                    _ptr(scores), _ptr(mui), _ptr(ws), wsb)
+                                    _ptr(scores), _ptr(mui))
     _lib.check(rc, "miner_score")
     return (scores, mui) if return_user else scores
 
@@ -214,8 +194,7 @@ def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly, contex
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32)
     with torch.cuda.device(history.device):
         rc = _lib.lib().miner_score(_stream(history.device), dt, _lib.SCORE_NONE, _ptr(history), _ptr(mask),
-                                    _ptr(his_bias), None, None, _ptr(pw.buf), B, L, 0, d, Dc, K, None, _ptr(mui),
-                                    None, 0)
+                                    _ptr(his_bias), None, None, _ptr(pw.buf), B, L, 0, d, Dc, K, None, _ptr(mui))
     _lib.check(rc, "miner_score(PolyAttention)")
     return mui
 

@@ -76,9 +76,9 @@ def test_argument_errors_before_any_launch(lib):
     assert lib.miner_pack_weights(None, _lib.DTYPE_BF16, None, None, None, 768, 200, 32, None) == -1
     assert lib.miner_pack_weights(None, 5, None, None, None, 768, 200, 32, None) == -1
     assert lib.miner_score(None, _lib.DTYPE_BF16, 9, None, None, None, None, None, None,
-                           1, 50, 40, 768, 200, 32, None, None, None, 0) == -1
+                           1, 50, 40, 768, 200, 32, None, None) == -1
     assert lib.miner_score(None, _lib.DTYPE_BF16, 0, None, None, None, None, None, None,
-                           1, 50, 40, 768, 200, 32, None, None, None, 0) == -1
+                           1, 50, 40, 768, 200, 32, None, None) == -1
     for code in (0, -1, -2, -3, -4):
         assert lib.miner_strerror(code)
 

@@ -16,9 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 STAMP_LIB = os.path.join(ROOT, "miner_amd", "libminer_hip_stamps.so")
 STAGES = ["S0 wait history DMA", "S1 W1·Eᵀ+tanh", "S2 Q·Pᵀ", "S3 softmax", "S4 A·E", "S5 W2+gelu", "S6 products", "S6 reduce", "S7 score", "loop tail"]
-PAIR_STAGES = ["S0 wait E(b0)", "S1(b0)", "S3(b0)+DMA E(b1)", "S4(b0)+scratch+wait", "S1(b1)", "S3+S4(b1)",
-               "S5 pair (+mui(b0) back)", "wait+DMA issue+GELU0->", "S6/S7(b0)", "S6/S7(b1)",
-               "am0+GELU1+park", "cand DMA issue+GELU0"]
+
 
 
 def build(extra=(), out=STAMP_LIB):
@@ -37,7 +35,6 @@ def main():
     ap.add_argument("--L", type=int, default=50)
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--C", type=int, default=40)
-    ap.add_argument("--pair", action="store_true", help="profile the pair kernel (workspace) instead")
     args = ap.parse_args()
     lib = STAMP_LIB if not args.variant else STAMP_LIB.replace(".so", "_" + args.variant.replace(",", "_").replace("=", "") + ".so")
     if args.build:
@@ -54,9 +51,7 @@ def main():
     imp = synthetic.impressions(36, 0, args.batch, L=args.L, d=args.d, C=args.C, device="cuda", dtype=dt)
     W1, Q, W2 = synthetic.init_weights(36, args.d, 200, 32, device="cuda")
     pw = ops.pack_weights(W1, Q, W2, dtype=dt)
-    # the stamps live in the single-impression kernel (no workspace); the pair kernel is timed beside
     for _ in range(2):
-        ops.score(imp.history, imp.his_mask, imp.candidates, pw, use_workspace=False)
         ops.score(imp.history, imp.his_mask, imp.candidates, pw)
     torch.cuda.synchronize()
     out = (ctypes.c_ulonglong * 16)()
@@ -68,19 +63,12 @@ def main():
         ops.score(imp.history, imp.his_mask, imp.candidates, pw)
     ev1.record()
     torch.cuda.synchronize()
-    print(f"pair kernel (no stamps): {ev0.elapsed_time(ev1) / reps:.3f} ms/launch")
-    fn(out)  # reset
-    ev0.record()
-    for _ in range(reps):
-        ops.score(imp.history, imp.his_mask, imp.candidates, pw, use_workspace=args.pair)
-    ev1.record()
-    torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / reps
-    names = PAIR_STAGES if args.pair else STAGES
+    names = STAGES
     assert fn(out) == 0
     n = out[12]
     tot = sum(out[i] for i in range(len(names)))
-    print(("PAIR " if args.pair else "SINGLE ") + f"{args.dtype} L={args.L} d={args.d} C={args.C} batch={args.batch}: {ms:.3f} ms/launch, "
+    print(f"{args.dtype} L={args.L} d={args.d} C={args.C} batch={args.batch}: {ms:.3f} ms/launch, "
           f"{n} impression-passes, {tot / n:.0f} cycles per impression per workgroup")
     for i, name in enumerate(names):
         print(f"  {name:22s} {out[i] / n:10.0f} cycles  {100.0 * out[i] / tot:5.1f}%")
