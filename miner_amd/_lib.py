@@ -18,7 +18,7 @@ SCORE_WEIGHTED, SCORE_MAX, SCORE_MEAN, SCORE_NONE = 0, 1, 2, 3
 SCORE_TYPES = {"weighted": SCORE_WEIGHTED, "max": SCORE_MAX, "mean": SCORE_MEAN, "none": SCORE_NONE}
 ABI_VERSION = 2
 
-# every symbol include/miner_score.h declares: name -> (restype, argtypes)
+# every symbol include/*.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 SIGNATURES = {
@@ -30,6 +30,8 @@ SIGNATURES = {
     "miner_lds_bytes": (_I, [_I, _I, _I, _I, _I]),
     "miner_strerror": (ctypes.c_char_p, [_I]),
     "miner_abi_version": (_I, []),
+    # include/miner_metrics.h
+    "miner_impression_metrics": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
 }
 
 _lib = None

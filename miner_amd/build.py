@@ -14,7 +14,9 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "miner_score.hip")
+SRC = os.path.join(HERE, "csrc", "miner_score.hip")      # the fused scoring kernel
+SOURCES = [SRC, os.path.join(HERE, "csrc", "miner_metrics.hip")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("miner_score.h", "miner_metrics.h")]
 LIB = os.path.join(HERE, "libminer_hip.so")
 ARCH = os.environ.get("MINER_OFFLOAD_ARCH", "gfx950")
 
@@ -27,13 +29,13 @@ def hipcc() -> str:
 
 
 def build_library(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/miner_score.hip -> miner_amd/libminer_hip.so (skipped when up to date)."""
-    deps = [SRC, os.path.join(ROOT, "include", "miner_score.h")]
+    """Compile csrc/*.hip -> miner_amd/libminer_hip.so (skipped when up to date)."""
+    deps = SOURCES + HEADERS
     if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(p) for p in deps):
         return LIB
     tmp = LIB + f".tmp{os.getpid()}"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), SRC, "-o", tmp]
+           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), *SOURCES, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)

@@ -122,6 +122,32 @@ def reduce_metrics(pairs: "evaluation.GroupedPairs", metrics: List[str], save_re
     return out
 
 
+def reduce_device_metrics(probs: torch.Tensor, labels: torch.Tensor, offsets: torch.Tensor, metrics: List[str],
+                          save_result: bool = False, path: str = None) -> Dict[str, float]:
+    """As ``reduce_metrics`` for device-resident (prob, label, offsets) of this rank's impressions,
+    with the per-impression metrics computed by the GPU kernel (miner_amd.metrics)."""
+    from . import metrics as gm
+    rank, ws = world()
+    per = gm.per_impression(probs, labels, offsets, [m for m in metrics if m != "auc"])
+    out = {}
+    for metric in metrics:
+        if metric == "auc":
+            sc = all_gather_concat(probs.double().reshape(-1))
+            lb = all_gather_concat(labels.reshape(-1).to(torch.uint8))
+            out["auc"] = evaluation.auc_score(lb.cpu().numpy(), sc.cpu().numpy())
+            continue
+        vals = per[metric]
+        ok = ~np.isnan(vals)
+        s, c = all_reduce_sum(np.array([vals[ok].sum(), ok.sum()], np.float64))
+        out[evaluation.metric_key(metric)] = float(s / c) if c > 0 else float("nan")
+        if save_result:
+            full = all_gather_concat(torch.from_numpy(vals)).cpu().numpy()
+            if rank == 0:
+                w = full.astype(int) if metric.startswith("hit") else full
+                evaluation.save_scores(os.path.join(path, evaluation.metric_file(metric)), w.tolist())
+    return out
+
+
 def reduce_eval_loss(partials: torch.Tensor) -> float:
     """Sum (numerator, positives) from evaluation.eval_loss_partials over ranks -> the eval loss."""
     num, pos = all_reduce_sum(partials.detach().cpu().numpy())

@@ -1,0 +1,130 @@
+"""GPU per-impression ranking metrics, behind the reference evaluator contract.
+
+``per_impression`` runs ``miner_impression_metrics`` (include/miner_metrics.h) over impressions in
+CSR layout: group AUC, MRR, nDCG@k and hit@k of every impression in one kernel. The reference's
+only order-dependent case — MRR / nDCG of an impression where a tie mixes a click and a non-click,
+ranked by numpy's ``argsort`` (src/evaluation.py:188, :208) — is flagged by the kernel and
+recomputed here on the host with the reference functions, so results equal the reference's.
+
+``compute_metrics`` returns the reference's metric dict (src/evaluation.py:36-84): the per-impression
+metrics nan-averaged, and the flattened global ``auc`` (:53-55) over all pairs. ``DeviceEvaluator``
+keeps (probability, label) on the device batch by batch; its ``compute_scores`` is the reference's
+``compute_scores`` and, under torch.distributed, reduces over ranks (miner_amd.distributed).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from . import _lib, evaluation
+
+
+def _ks(metrics: Sequence[str]) -> List[int]:
+    return sorted({int(m.split("@")[1]) for m in metrics if m.startswith(("ndcg@", "hit@"))})
+
+
+def per_impression(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: Sequence[str]) -> Dict[str, np.ndarray]:
+    """probs [N] (ranked values, fp32), labels [N] (0/1), offsets [G+1] int32 — device tensors.
+
+    Returns {metric: float64 array [G]} for every per-impression metric named in ``metrics``
+    (group_auc, mrr, ndcg@k, hit@k); impression g owns [offsets[g], offsets[g+1]).
+    """
+    for t in (probs, labels, offsets):
+        if t.device.type != "cuda":
+            raise RuntimeError("miner_amd.metrics runs on the GPU only (no CPU fallback)")
+    probs = probs.reshape(-1).to(torch.float32).contiguous()
+    lab = labels.reshape(-1).to(torch.uint8).contiguous()
+    offs = offsets.to(torch.int32).contiguous()
+    G = offs.numel() - 1
+    ks = _ks(metrics)
+    if len(ks) > 8:
+        raise ValueError("at most 8 distinct @k cut-offs per call")
+    nk = len(ks)
+    out = torch.empty((max(G, 0), 2 + 2 * nk), dtype=torch.float64, device=probs.device)
+    mixed = torch.empty((max(G, 0),), dtype=torch.uint8, device=probs.device)
+    karr = (np.ctypeslib.ctypes.c_int32 * max(nk, 1))(*ks)
+    with torch.cuda.device(probs.device):
+        rc = _lib.lib().miner_impression_metrics(torch.cuda.current_stream(probs.device).cuda_stream,
+                                                 probs.data_ptr(), lab.data_ptr(), offs.data_ptr(), G,
+                                                 karr, nk, out.data_ptr(), mixed.data_ptr())
+    _lib.check(rc, "miner_impression_metrics")
+    res = out.cpu().numpy()
+    mix = np.flatnonzero(mixed.cpu().numpy())
+    if mix.size:   # the reference's argsort order among mixed-label ties: host recompute
+        o = offs.cpu().numpy()
+        for g in mix:
+            p = probs[o[g]:o[g + 1]].double().cpu().numpy()
+            y = lab[o[g]:o[g + 1]].cpu().numpy().astype(np.int64)
+            res[g, 1] = evaluation.compute_mrr_score(y, p)
+            for t, k in enumerate(ks):
+                res[g, 2 + t] = evaluation.compute_ndcg_score(y, p, k)
+    cols = {"group_auc": res[:, 0], "mrr": res[:, 1]}
+    for t, k in enumerate(ks):
+        cols[f"ndcg@{k}"] = res[:, 2 + t]
+        cols[f"hit@{k}"] = res[:, 2 + nk + t]
+    return {m: cols[evaluation.metric_key(m)] for m in metrics if m != "auc"}
+
+
+def compute_metrics(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: List[str], save_result: bool = False,
+                    path: str = None) -> Dict[str, float]:
+    """The reference's metric dict (src/evaluation.py:36-84) for impressions already sorted by id."""
+    per = per_impression(probs, labels, offsets, metrics)
+    out = {}
+    for m in metrics:
+        if m == "auc":
+            out["auc"] = evaluation.auc_score(labels.reshape(-1).cpu().numpy(), probs.reshape(-1).double().cpu().numpy())
+            continue
+        vals = per[m]
+        out[evaluation.metric_key(m)] = float(np.nanmean(vals))
+        if save_result:
+            w = vals.astype(int) if m.startswith("hit") else vals
+            evaluation.save_scores(os.path.join(path, evaluation.metric_file(m)), w.tolist())
+    return out
+
+
+class DeviceEvaluator:
+    """Batched-layout evaluator with device-resident accumulation.
+
+    ``add(scores, labels, impression_ids, cand_offsets=None)`` takes the kernel's logits (dense
+    [B,C] or ragged [N] + offsets) on the device and keeps sigmoid(logits) (evaluation.py:165) and the
+    labels there; ``compute_scores(metrics, save_result, path)`` orders impressions by id
+    (evaluation.py:124, :143), runs the GPU metrics and, under torch.distributed, reduces over ranks
+    (each rank holding a contiguous id range).
+    """
+
+    def __init__(self):
+        self._probs, self._labels, self._sizes, self._ids = [], [], [], []
+
+    def add(self, scores: Tensor, labels: Tensor, impression_ids: Tensor, cand_offsets: Tensor = None):
+        self._probs.append(torch.sigmoid(scores.float()).reshape(-1))
+        self._labels.append(labels.reshape(-1).to(device=scores.device, dtype=torch.uint8))
+        if cand_offsets is None:
+            self._sizes.append(torch.full((scores.shape[0],), scores.shape[1], device=scores.device, dtype=torch.int64))
+        else:
+            self._sizes.append(torch.diff(cand_offsets.to(device=scores.device, dtype=torch.int64)))
+        self._ids.append(impression_ids.reshape(-1).to(device=scores.device, dtype=torch.int64))
+
+    def arrays(self):
+        probs = torch.cat(self._probs)
+        lab = torch.cat(self._labels)
+        sizes = torch.cat(self._sizes)
+        ids = torch.cat(self._ids)
+        order = torch.argsort(ids, stable=True)
+        offs = torch.zeros(sizes.numel() + 1, dtype=torch.int64, device=sizes.device)
+        offs[1:] = torch.cumsum(sizes, 0)
+        if not torch.equal(order, torch.arange(order.numel(), device=order.device)):
+            idx = torch.cat([torch.arange(int(offs[i]), int(offs[i + 1]), device=probs.device) for i in order.tolist()])
+            probs, lab, sizes = probs[idx], lab[idx], sizes[order]
+            offs[1:] = torch.cumsum(sizes, 0)
+        return probs, lab, offs.to(torch.int32)
+
+    def compute_scores(self, metrics: List[str], save_result: bool = False, path: str = None) -> Dict[str, float]:
+        from . import distributed
+        probs, lab, offs = self.arrays()
+        if distributed.world()[1] == 1:
+            return compute_metrics(probs, lab, offs, metrics, save_result, path)
+        return distributed.reduce_device_metrics(probs, lab, offs, metrics, save_result, path)

@@ -10,13 +10,16 @@ import torch
 from miner_amd import _lib, ops
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "miner_score.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 
 
 def declared_symbols():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(miner_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for path in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
+        names |= set(re.findall(r"\b(miner_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")

@@ -20,9 +20,9 @@ STAGES = ["S0 wait history DMA", "S1 W1·Eᵀ+tanh", "S2 Q·Pᵀ", "S3 softmax",
 
 
 def build(extra=(), out=STAMP_LIB):
-    from miner_amd.build import hipcc, SRC, ARCH
+    from miner_amd.build import hipcc, SOURCES, ARCH
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMINER_STAMPS",
-           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), *extra, SRC, "-o", out]
+           "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), *extra, *SOURCES, "-o", out]
     subprocess.run(cmd, check=True)
 
 
