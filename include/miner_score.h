@@ -96,6 +96,22 @@ int miner_score(void* stream, int dtype, int score_type,
                 float* scores, float* user_out);
 
 /*
+ * miner_score with the news rows gathered by id from a device news-embedding table:
+ *   news_table [n_news, d] dtype  the news encoder's output for every news item, computed once
+ *                                 (the reference re-encodes each sample's news through
+ *                                 Miner.forward, model.py:104-111, fed by reader.py:366-379 and
+ *                                 entities.py:375-411)
+ *   his_ids    [B, L]      int32  table rows of the (left-padded) history; the pad news is a row
+ *   cand_ids   [sum C_b]   int32  table rows of the candidates (CSR by cand_offsets, or [B, C])
+ * Everything else as miner_score. Ids outside [0, n_news) are clamped (never read out of bounds);
+ * the Python wrapper validates them and raises.
+ */
+int miner_score_gather(void* stream, int dtype, int score_type, const void* news_table, int n_news,
+                       const int32_t* his_ids, const uint8_t* his_mask, const float* his_bias,
+                       const int32_t* cand_ids, const int32_t* cand_offsets, const void* packed_weights,
+                       int B, int L, int C, int d, int Dc, int K, float* scores, float* user_out);
+
+/*
  * TargetAwareAttention.forward (model.py:200-216) on its own:
  *   query [B, K, d] dtype (multi_user_interest), key [sum C_b, d] dtype (candidates),
  *   value [sum C_b, K] fp32 (matching scores Cand·muiᵀ), packed_weights with w_target packed

@@ -25,6 +25,7 @@ SIGNATURES = {
     "miner_packed_weights_bytes": (ctypes.c_size_t, [_I, _I, _I, _I]),
     "miner_pack_weights": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _P]),
     "miner_score": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "miner_score_gather": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "miner_target_aware": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "miner_supported": (_I, [_I, _I, _I, _I, _I]),
     "miner_lds_bytes": (_I, [_I, _I, _I, _I, _I]),

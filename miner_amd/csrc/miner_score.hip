@@ -93,6 +93,10 @@ struct Params {
   int MS;       // mui row stride
   int PS;       // P row stride (elements)
   int offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux;
+  // news-table gather mode (miner_score_gather): hist and cand point to the table [n_news, d]
+  const int32_t* his_ids;    // [B, L] rows of the table, or null (dense history)
+  const int32_t* cand_ids;   // [sum C_b] rows of the table, or null (dense candidates)
+  int n_news;
   int eimg;     // bytes of the history image (bf16): the candidate rows may be staged there
   int dbg;      // ablation bits, honoured only by the -DMINER_STAMPS diagnostic build
 };
@@ -321,8 +325,11 @@ __device__ __forceinline__ void dma_b32(const void* g, unsigned lds) {
 }
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // nrows rows of d elements -> the swizzled image (whole 1 KiB blocks, one per wave-instruction)
+// Gather mode: row r is table row ids[r] (ids in LDS), clamped to [0, n_news) so a bad id can
+// never address outside the table (the host wrapper validates ids and raises).
 template <class T>
-__device__ __forceinline__ void dma_rows(const T* src, int nrows, int d, char* img, int wave, int lane) {
+__device__ __forceinline__ void dma_rows(const T* src, int nrows, int d, char* img, int wave, int lane,
+                                         const int32_t* idsL = nullptr, int n_news = 0) {
   const int cpr = d >> 3;                 // 16-byte chunks per row
   const int g16 = (cpr & 15) == 0;
   const int total = nrows * cpr;
@@ -331,21 +338,32 @@ __device__ __forceinline__ void dma_rows(const T* src, int nrows, int d, char* i
     const int pos = blk * 64 + lane;
     const int row = pos / cpr;
     const int c = pos - row * cpr;
-    const T* g = (pos < total) ? src + (size_t)row * d + (size_t)((c ^ eswz(row, g16)) << 3) : src;
+    const size_t r = idsL ? (size_t)min(max(idsL[min(row, nrows - 1)], 0), n_news - 1) : (size_t)row;
+    const T* g = (pos < total) ? src + r * d + (size_t)((c ^ eswz(row, g16)) << 3) : src;
     dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
   }
 }
 
-// impression b's mask bytes (as the aligned words covering them) and fp32 bias -> the aux block
-__device__ __forceinline__ void dma_aux(const uint8_t* mask, const float* bias, int B, int L, int b, char* aux,
-                                        int wave, int lane) {
+// Per-impression aux block (1 KiB): [0,256) the mask bytes (as the aligned words covering them),
+// [256,512) fp32 bias, [512,768) history ids, [768,1024) the first 64 candidate ids (gather mode)
+constexpr int kAuxBytes = 1024;
+template <class P>
+__device__ __forceinline__ void dma_aux(const P& p, int b, char* aux, int wave, int lane) {
+  const int L = p.L;
   if (wave == 0) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(mask + (size_t)b * L) & ~(uintptr_t)3;
-    const uintptr_t last = reinterpret_cast<uintptr_t>(mask + (size_t)B * L - 1) & ~(uintptr_t)3;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + (size_t)b * L) & ~(uintptr_t)3;
+    const uintptr_t last = reinterpret_cast<uintptr_t>(p.mask + (size_t)p.B * L - 1) & ~(uintptr_t)3;
     const uintptr_t w = a + 4 * (uintptr_t)lane;
     dma_b32(reinterpret_cast<const void*>(w < last ? w : last), __builtin_amdgcn_readfirstlane(lds_offset(aux)));
-  } else if (wave == 1 && bias) {
-    dma_b32(bias + (size_t)b * L + min(lane, L - 1), __builtin_amdgcn_readfirstlane(lds_offset(aux + 256)));
+  } else if (wave == 1 && p.bias) {
+    dma_b32(p.bias + (size_t)b * L + min(lane, L - 1), __builtin_amdgcn_readfirstlane(lds_offset(aux + 256)));
+  } else if (wave == 2 && p.his_ids) {
+    dma_b32(p.his_ids + (size_t)b * L + min(lane, L - 1), __builtin_amdgcn_readfirstlane(lds_offset(aux + 512)));
+  } else if (wave == 3 && p.cand_ids) {
+    const int cb = p.cand_off ? p.cand_off[b] : b * p.C;
+    const int n = p.cand_off ? p.cand_off[b + 1] - cb : p.C;
+    if (n > 0)
+      dma_b32(p.cand_ids + cb + min(lane, n - 1), __builtin_amdgcn_readfirstlane(lds_offset(aux + 768)));
   }
 }
 
@@ -450,7 +468,7 @@ template <class T, int NM, bool WEIGHTED, bool FULL>
 __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
                                             const Frag<T> (&amr)[kMaxJ], const T* __restrict__ cand,
                                             const char* cimg, int Cb, int cc, int d, int wave, int r, int h,
-                                            const T* muiL, int msE) {
+                                            const T* muiL, int msE, const int32_t* cids, int n_news) {
   // mui fragments of the wave's d-tiles: bf16 preloads them (amr) before the chunk loop, because
   // the partial slabs overwrite mui; fp32 reads them here
   Frag<T> am[NM];
@@ -474,8 +492,9 @@ __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], co
           frag_load_E(reinterpret_cast<Frag<__bf16>&>(bc[m]), cimg, c, (wave + kWaves * m) * 32, h, d * 2, g16);
       }
     }
-    if (!cimg || sizeof(T) != 2) {
-      const T* crow = cand + (size_t)c * d + 16 * h;
+    if (!cimg || sizeof(T) != 2) {   // gather mode: table row cids[c] (ids from global)
+      const size_t cr = cids ? (size_t)min(max(cids[c], 0), n_news - 1) : (size_t)c;
+      const T* crow = cand + cr * d + 16 * h;
 #pragma unroll
       for (int m = 0; m < NM; ++m) frag_load_stream(bc[m], crow + (wave + kWaves * m) * 32);
     }
@@ -492,10 +511,11 @@ __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], co
 template <class T, bool WEIGHTED, bool FULL>
 __device__ __forceinline__ void s6_dispatch(int nm, f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
                                             const Frag<T> (&am)[kMaxJ], const T* cand, const char* cimg, int Cb,
-                                            int cc, int d, int wave, int r, int h, const T* muiL, int msE) {
-  if (nm == 3) s6_products<T, 3, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
-  else if (nm == 2) s6_products<T, 2, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
-  else if (nm == 1) s6_products<T, 1, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
+                                            int cc, int d, int wave, int r, int h, const T* muiL, int msE,
+                                            const int32_t* cids, int n_news) {
+  if (nm == 3) s6_products<T, 3, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
+  else if (nm == 2) s6_products<T, 2, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
+  else if (nm == 1) s6_products<T, 1, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
 }
 
 // one 32x32 accumulator tile -> rows [c][k] of a partial slab (4 x 16-byte stores per lane):
@@ -600,10 +620,13 @@ __device__ __forceinline__ float s7_score(const float (&lgv)[4], const float (&m
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
 // ---------------------------------------------------------------------------------------------
-template <class T, int MODE, int NS>
+template <class T, int MODE, int NS, bool GATHER>
 __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kBf16 = sizeof(T) == 2;
+  // news-table gather mode (compile-time, so the dense instantiations carry no gather code)
+  const int32_t* const his_ids = GATHER ? p.his_ids : nullptr;
+  const int32_t* const cand_ids = GATHER ? p.cand_ids : nullptr;
   constexpr bool kDma = kBf16 && MODE == kFull;  // history staged in LDS by DMA
 #ifndef MINER_PF
 #define MINER_PF 3
@@ -634,9 +657,12 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
     FRESH_LANE_IDS();
     if constexpr (kDma) {
       if (tid < 4) reinterpret_cast<u32x4*>(smem + p.offZ)[tid] = u32x4{0u, 0u, 0u, 0u};
-      if (blockIdx.x < p.B) {
-        dma_rows(static_cast<const T*>(p.hist) + (size_t)blockIdx.x * L * d, L, d, ldsE, wave, lane);
-        dma_aux(p.mask, p.bias, p.B, L, blockIdx.x, smem + p.offAux, wave, lane);
+      if (blockIdx.x < p.B) {   // aux (ids) first: the gathered history DMA reads them
+        dma_aux(p, blockIdx.x, smem + p.offAux, wave, lane);
+        vm_wait_all();
+        __syncthreads();
+        dma_rows(static_cast<const T*>(p.hist) + (his_ids ? 0 : (size_t)blockIdx.x * L * d), L, d, ldsE, wave, lane,
+                 his_ids ? reinterpret_cast<const int32_t*>(smem + p.offAux + 512) : nullptr, p.n_news);
       }
     }
     if constexpr (!kBf16)
@@ -649,13 +675,28 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
     ++n_done;
     const int cbase = p.cand_off ? p.cand_off[b] : b * p.C;
     const int Cb = p.cand_off ? (p.cand_off[b + 1] - cbase) : p.C;
-    const T* __restrict__ cand = static_cast<const T*>(p.cand) + (DBG(2) ? (size_t)0 : (size_t)cbase * d);
+    // gather mode: cand = the table, cids = this impression's candidate ids (global)
+    const int32_t* cids = cand_ids ? cand_ids + cbase : nullptr;
+    const T* __restrict__ cand = static_cast<const T*>(p.cand) + ((DBG(2) || cids) ? (size_t)0 : (size_t)cbase * d);
     const int bnext = b + gridDim.x;
     bool prefetched = false;   // next impression's history DMA already issued
     const char* cimg = nullptr;   // candidate rows staged in the history image (bf16)
+    // aux blocks alternate by iteration: the next impression's aux lands while this one's is read
+    char* aux = smem + p.offAux + ((n_done - 1) & 1) * kAuxBytes;
+    char* auxn = smem + p.offAux + (n_done & 1) * kAuxBytes;
 
     if constexpr (MODE == kFull) {
-      const T* __restrict__ E = static_cast<const T*>(p.hist) + (size_t)b * L * d;
+      const T* __restrict__ E = static_cast<const T*>(p.hist) + (his_ids ? 0 : (size_t)b * L * d);
+      // fp32 path: history row l (gather mode: table row his_ids[b][l], staged in LDS below)
+      const int32_t* hidL = reinterpret_cast<const int32_t*>(smem + p.offAux);
+      auto erow = [&](int l) -> const T* {
+        return his_ids ? E + (size_t)min(max(hidL[l], 0), p.n_news - 1) * d : E + (size_t)l * d;
+      };
+      if constexpr (!kBf16 && GATHER) {
+        FRESH_LANE_IDS();
+        __syncthreads();   // the previous impression's readers of the id block are done
+        if (tid < L) reinterpret_cast<int32_t*>(smem + p.offAux)[tid] = his_ids[(size_t)b * L + tid];
+      }
       T* Ps = reinterpret_cast<T*>(smem + p.offP);         // P[l][c], row stride PS (aliases mui)
       float* S = reinterpret_cast<float*>(smem + p.offS);  // Sᵀ[k][l], [32][kMaxL] (aliases mui)
       T* Aw = reinterpret_cast<T*>(smem + p.offAw);        // A[k][l], [32][AwS]
@@ -690,8 +731,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
                 frag_load_E(b0, ldsE, l0, kk, h, rowB, g16);
                 frag_load_E(b1, ldsE, l1, kk, h, rowB, g16);
               } else {
-                frag_load(b0, E + (size_t)l0 * d + kk + 16 * h);
-                frag_load(b1, E + (size_t)l1 * d + kk + 16 * h);
+                frag_load(b0, erow(l0) + kk + 16 * h);
+                frag_load(b1, erow(l1) + kk + 16 * h);
               }
               mma_slab<T>(acc0, ring[s], b0);
               mma_slab<T>(acc1, ring[s], b1);
@@ -708,8 +749,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
                 frag_load_E(b0, ldsE, l0, kk, h, rowB, g16);
                 frag_load_E(b1, ldsE, l1, kk, h, rowB, g16);
               } else {
-                frag_load(b0, E + (size_t)l0 * d + kk + 16 * h);
-                frag_load(b1, E + (size_t)l1 * d + kk + 16 * h);
+                frag_load(b0, erow(l0) + kk + 16 * h);
+                frag_load(b1, erow(l1) + kk + 16 * h);
               }
               mma_slab<T>(acc0, ring[s], b0);
               mma_slab<T>(acc1, ring[s], b1);
@@ -784,7 +825,6 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         }
         float v[4] = {sv.x, sv.y, sv.z, sv.w};
         float mx = -INFINITY;
-        const char* aux = smem + p.offAux;
         const int shift = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)b * L) & 3);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -874,7 +914,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {   // rows >= L: finite data times a zero weight
                   const int l = min(lb + 16 * h + e, L - 1);
-                  bf.q[e >> 2][e & 3] = __float_as_uint(E[(size_t)l * d + i0 + r]);
+                  bf.q[e >> 2][e & 3] = __float_as_uint(erow(l)[i0 + r]);
                 }
               }
               if constexpr (kBf16) mma_slab<T>(acc, bf, ls == 0 ? af0 : af1);   // muiᵀ = Eᵀ·Aᵀ
@@ -906,11 +946,14 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         // This impression's candidate rows -> the (dead) history image, landing during S5.  Issued
         // before S5's ring: an untracked DMA issued inside the ring, older than later ring loads,
         // would make each of their waits cover its HBM latency too (measured: S5 +6K cycles).
+        FRESH_LANE_IDS();
         if (need_scores && Cb > 0 && Cb <= kCChunk && ((Cb * rowB + 1023) & ~1023) <= p.eimg) {
-          FRESH_LANE_IDS();
-          dma_rows(cand, Cb, d, ldsE, wave, lane);
+          dma_rows(cand, Cb, d, ldsE, wave, lane, cids ? reinterpret_cast<const int32_t*>(aux + 768) : nullptr,
+                   p.n_news);
           cimg = ldsE;
         }
+        // the next impression's mask / bias / ids -> the other aux block (read by its DMAs and S3)
+        if (bnext < p.B) dma_aux(p, bnext, auxn, wave, lane);
       }
       STAMP(4);
     } else {  // MODE == kTaa: multi_user_interest comes from global (query)
@@ -958,16 +1001,18 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           const int nm = (ns - wave + kWaves - 1) / kWaves;
           f32x16 lg[2], mt[2];
           lg[0] = lg[1] = mt[0] = mt[1] = zero16();
-          if (weighted) s6_dispatch<T, true, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
-          else s6_dispatch<T, false, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE);
+          if (weighted) s6_dispatch<T, true, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
+          else s6_dispatch<T, false, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
           STAMP_SYNC();
           STAMP(6);
           if constexpr (kDma) {
-            // the partial slabs overwrite mui; every wave is done with mui and the candidate image
+            // the partial slabs overwrite mui; every wave is done with mui and the candidate image;
+            // the next impression's aux (its history ids) has landed for every wave
+            vm_wait_all();
             __syncthreads();
             if (cimg && bnext < p.B && !DBG(4)) {   // single chunk: next impression's history now
-              dma_rows(static_cast<const T*>(p.hist) + (size_t)bnext * L * d, L, d, ldsE, wave, lane);
-              dma_aux(p.mask, p.bias, p.B, L, bnext, smem + p.offAux, wave, lane);
+              dma_rows(static_cast<const T*>(p.hist) + (his_ids ? 0 : (size_t)bnext * L * d), L, d, ldsE, wave, lane,
+                       his_ids ? reinterpret_cast<const int32_t*>(auxn + 512) : nullptr, p.n_news);
               prefetched = true;
             }
           }
@@ -1028,8 +1073,10 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
     if constexpr (kDma) {
       FRESH_LANE_IDS();
       if (!prefetched && bnext < p.B && !DBG(4)) {   // the history region is free now
-        dma_rows(static_cast<const T*>(p.hist) + (size_t)bnext * L * d, L, d, ldsE, wave, lane);
-        dma_aux(p.mask, p.bias, p.B, L, bnext, smem + p.offAux, wave, lane);
+        vm_wait_all();
+        __syncthreads();   // the next impression's aux (history ids) landed for every wave
+        dma_rows(static_cast<const T*>(p.hist) + (his_ids ? 0 : (size_t)bnext * L * d), L, d, ldsE, wave, lane,
+                 his_ids ? reinterpret_cast<const int32_t*>(auxn + 512) : nullptr, p.n_news);
       }
     }
     STAMP(9);
@@ -1116,8 +1163,8 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
     c.offPart = 0;                                  // TAA: [partial slabs | mui]
     const int r1 = mode == kFull ? eimg : parts;
     c.offZ = round16(r1);
-    c.offAux = c.offZ + 64;                         // mask words (256 B) + bias (256 B)
-    off = mode == kFull ? c.offAux + 512 : c.offZ;
+    c.offAux = c.offZ + 64;                         // 2 aux blocks (mask | bias | ids), by parity
+    off = mode == kFull ? c.offAux + 2 * kAuxBytes : c.offZ;
     c.offLg = c.offMt = 0;
   } else {
     c.offE = c.offZ = c.offPart = 0;
@@ -1131,6 +1178,10 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   if (bf && mode == kFull) c.offPart = c.offMui;   // full: after S6 products mui is dead
   c.offAw = round16(c.offMui + r2);
   c.total = c.offAw + aw;
+  if (!bf && mode == kFull) {   // fp32 gather mode: the impression's history ids
+    c.offAux = round16(c.total);
+    c.total = c.offAux + kMaxL * 4;
+  }
   return c;
 }
 
@@ -1158,9 +1209,9 @@ int num_cus() {
 
 inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <class T, int MODE, int NS>
+template <class T, int MODE, int NS, bool GATHER = false>
 int launch(void* stream, const Params& prm, int lds) {
-  auto kern = miner_fused<T, MODE, NS>;
+  auto kern = miner_fused<T, MODE, NS, GATHER>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   const int per_cu = kLdsMax / lds > 0 ? (kLdsMax / lds > 2 ? 2 : kLdsMax / lds) : 1;
@@ -1179,19 +1230,24 @@ int run(void* stream, int dtype, int mode, Params prm) {
   prm.MS = c.MS; prm.PS = c.PS; prm.offE = c.offE; prm.offZ = c.offZ; prm.offP = c.offP; prm.offS = c.offS;
   prm.offMui = c.offMui; prm.offAw = c.offAw; prm.offPart = c.offPart; prm.offLg = c.offLg; prm.offMt = c.offMt;
   prm.offAux = c.offAux; prm.eimg = c.eimg;
+  const bool gather = prm.his_ids != nullptr;
   if (dtype == MINER_DTYPE_BF16) {
     // bf16 kernels specialised on the embedding dim (d = 32*NS) so the slab loops fully unroll
     switch (prm.d) {
-#define MINER_NS_CASE(ns) \
-  case 32 * ns: return mode == kFull ? launch<__bf16, kFull, ns>(stream, prm, c.total) : launch<__bf16, kTaa, ns>(stream, prm, c.total);
+#define MINER_NS_CASE(ns)                                                                        \
+  case 32 * ns:                                                                                  \
+    if (mode == kTaa) return launch<__bf16, kTaa, ns>(stream, prm, c.total);                     \
+    return gather ? launch<__bf16, kFull, ns, true>(stream, prm, c.total) : launch<__bf16, kFull, ns>(stream, prm, c.total);
       MINER_NS_CASE(2) MINER_NS_CASE(4) MINER_NS_CASE(6) MINER_NS_CASE(8) MINER_NS_CASE(12)
       MINER_NS_CASE(16) MINER_NS_CASE(24)
 #undef MINER_NS_CASE
       default:
-        return mode == kFull ? launch<__bf16, kFull, 0>(stream, prm, c.total) : launch<__bf16, kTaa, 0>(stream, prm, c.total);
+        if (mode == kTaa) return launch<__bf16, kTaa, 0>(stream, prm, c.total);
+        return gather ? launch<__bf16, kFull, 0, true>(stream, prm, c.total) : launch<__bf16, kFull, 0>(stream, prm, c.total);
     }
   }
-  return mode == kFull ? launch<float, kFull, 0>(stream, prm, c.total) : launch<float, kTaa, 0>(stream, prm, c.total);
+  if (mode == kTaa) return launch<float, kTaa, 0>(stream, prm, c.total);
+  return gather ? launch<float, kFull, 0, true>(stream, prm, c.total) : launch<float, kFull, 0>(stream, prm, c.total);
 }
 
 size_t packed_bytes(int dtype, int d, int Dc) {
@@ -1247,6 +1303,28 @@ int miner_score(void* stream, int dtype, int score_type, const void* history, co
   prm.hist = history; prm.mask = his_mask; prm.bias = his_bias; prm.cand = candidates;
   prm.cand_off = cand_offsets; prm.wp = packed_weights; prm.value = nullptr; prm.scores = scores;
   prm.mui_out = user_out;
+  prm.B = B; prm.L = L; prm.C = C; prm.d = d; prm.Dc = Dc; prm.K = K; prm.score_type = score_type;
+  return run(stream, dtype, kFull, prm);
+}
+
+int miner_score_gather(void* stream, int dtype, int score_type, const void* news_table, int n_news,
+                       const int32_t* his_ids, const uint8_t* his_mask, const float* his_bias,
+                       const int32_t* cand_ids, const int32_t* cand_offsets, const void* packed_weights,
+                       int B, int L, int C, int d, int Dc, int K, float* scores, float* user_out) {
+  if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
+  if (B < 0 || C < 0 || n_news <= 0) return MINER_EINVAL;
+  const int sh = check_shape(dtype, kFull, L, d, Dc, K);
+  if (sh != MINER_OK) return sh;
+  if (!news_table || !his_ids || !his_mask || !packed_weights) return MINER_EINVAL;
+  if (score_type != MINER_SCORE_NONE && (!cand_ids || !scores)) return MINER_EINVAL;
+  if (score_type == MINER_SCORE_NONE && !user_out) return MINER_EINVAL;
+  if (!aligned16(news_table) || !aligned16(packed_weights)) return MINER_EALIGN;
+  if (B == 0) return MINER_OK;
+  Params prm{};
+  prm.hist = news_table; prm.mask = his_mask; prm.bias = his_bias; prm.cand = news_table;
+  prm.cand_off = cand_offsets; prm.wp = packed_weights; prm.value = nullptr; prm.scores = scores;
+  prm.mui_out = user_out; prm.his_ids = his_ids; prm.cand_ids = score_type != MINER_SCORE_NONE ? cand_ids : nullptr;
+  prm.n_news = n_news;
   prm.B = B; prm.L = L; prm.C = C; prm.d = d; prm.Dc = Dc; prm.K = K; prm.score_type = score_type;
   return run(stream, dtype, kFull, prm);
 }

@@ -172,6 +172,79 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
     return (scores, mui) if return_user else scores
 
 
+def _check_ids(ids: torch.Tensor, n: int, what: str) -> None:
+    if ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= n):
+        raise ValueError(f"{what} must index the news table [0, {n})")
+
+
+def score_gather(news_table: torch.Tensor, his_ids: torch.Tensor, his_mask: torch.Tensor, cand_ids: torch.Tensor,
+                 w_poly, context_codes: torch.Tensor | None = None, w_target: torch.Tensor | None = None, *,
+                 score_type: str = "weighted", cand_offsets: torch.Tensor | None = None,
+                 his_bias: torch.Tensor | None = None, return_user: bool = False, validate: bool = True):
+    """``score`` with the news rows gathered by id from a device news-embedding table.
+
+    news_table [n_news, d] (the news encoder's output for every news item, float32 or bfloat16),
+    his_ids [B, L] int, his_mask [B, L] bool, cand_ids [B, C] (dense) or [N] with cand_offsets [B+1].
+    The reference re-encodes every sample's news (src/model/model.py:104-111 fed by
+    src/reader.py:366-379); with the table computed once, the kernel DMAs the rows by id.
+    Returns what ``score`` returns. ``validate`` checks ids / offsets on the device first.
+    """
+    st = _lib.SCORE_TYPES.get(score_type)
+    if st is None or st == _lib.SCORE_NONE:
+        raise ValueError("Invalid method of aggregating matching score")  # model.py:136
+    _require_device(news_table, his_ids, his_mask, cand_ids, context_codes, w_target, cand_offsets, his_bias)
+    if not isinstance(w_poly, PackedWeights):
+        _require_device(w_poly)
+    tdt = news_table.dtype
+    dt = _dtype_code(tdt)
+    table = _contig(news_table)
+    n_news, d = table.shape
+    B, L = his_ids.shape
+    hid = _contig(his_ids, torch.int32)
+    if isinstance(w_poly, PackedWeights):
+        Dc, K = w_poly.Dc, w_poly.K
+    else:
+        K, Dc = context_codes.shape
+    code = _lib.lib().miner_supported(dt, L, d, Dc, K)
+    if code != 0:
+        raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
+    pw = _as_packed(w_poly, context_codes, w_target if st == _lib.SCORE_WEIGHTED else None, tdt)
+    if st == _lib.SCORE_WEIGHTED and not pw.has_target:
+        raise ValueError("score_type='weighted' needs weights packed with w_target")
+    mask = _contig(his_mask)
+    if mask.dtype != torch.bool:
+        mask = mask != 0
+    if tuple(mask.shape) != (B, L):
+        raise ValueError(f"his_mask must be [{B},{L}]")
+    mask = mask.view(torch.uint8)
+    if his_bias is not None:
+        his_bias = _contig(his_bias, torch.float32)
+    if cand_offsets is None:
+        if cand_ids.dim() != 2 or cand_ids.shape[0] != B:
+            raise ValueError(f"dense cand_ids must be [{B},C]")
+        C = cand_ids.shape[1]
+        cid = _contig(cand_ids, torch.int32)
+        scores = torch.empty((B, C), device=table.device, dtype=torch.float32)
+        offs = None
+    else:
+        cid = _contig(cand_ids.reshape(-1), torch.int32)
+        offs = _contig(cand_offsets, torch.int32)
+        if validate:
+            check_offsets(offs, B, cid.numel())
+        C = 0
+        scores = torch.empty((cid.numel(),), device=table.device, dtype=torch.float32)
+    if validate:
+        _check_ids(hid, n_news, "his_ids")
+        _check_ids(cid, n_news, "cand_ids")
+    mui = torch.empty((B, K, d), device=table.device, dtype=torch.float32) if return_user else None
+    with torch.cuda.device(table.device):
+        rc = _lib.lib().miner_score_gather(_stream(table.device), dt, st, _ptr(table), n_news, _ptr(hid), _ptr(mask),
+                                           _ptr(his_bias), _ptr(cid), _ptr(offs), _ptr(pw.buf), B, L, C, d, Dc, K,
+                                           _ptr(scores), _ptr(mui))
+    _lib.check(rc, "miner_score_gather")
+    return (scores, mui) if return_user else scores
+
+
 def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly, context_codes: torch.Tensor | None = None,
                    his_bias: torch.Tensor | None = None) -> torch.Tensor:
     """PolyAttention.forward (src/model/model.py:159-185) -> mui [B,K,d] fp32."""
