@@ -120,3 +120,61 @@ def init_weights(seed: int, d: int, Dc: int, K: int, device="cpu"):
     bq = gain * (6.0 / (Dc + K)) ** 0.5
     Q = (torch.rand((K, Dc), generator=g) * 2 - 1) * bq
     return W1.to(device), Q.to(device), W2.to(device)
+
+
+@dataclasses.dataclass
+class Behaviors:
+    """Impressions as news ids (the reference's eval layout before the news encoder)."""
+    his_ids: torch.Tensor        # [n, L] int32 rows of the news table (left pad = row 0, the pad news)
+    his_mask: torch.Tensor       # [n, L] bool
+    cand_ids: torch.Tensor       # [N] int32
+    cand_offsets: torch.Tensor   # [n+1] int32
+    labels: torch.Tensor         # [N] uint8
+    impression_ids: torch.Tensor  # [n] int64
+
+    @property
+    def n(self) -> int:
+        return self.his_ids.shape[0]
+
+
+def news_table(seed: int, n_news: int, d: int, device="cpu", dtype=torch.float32) -> torch.Tensor:
+    """[n_news, d] news embeddings ~ N(0,1)/sqrt(d); row 0 is the pad news (reader.py:101-110)."""
+    g = torch.Generator(device="cpu").manual_seed(_mix(seed, 2**42))
+    return (torch.randn((n_news, d), generator=g) / d ** 0.5).to(device=device, dtype=dtype)
+
+
+def behaviors(seed: int, start: int, count: int, *, L: int, n_news: int, C=40, ragged=None,
+              device="cpu") -> Behaviors:
+    """Impressions [start, start+count): ids drawn per BLOCK of impressions from (seed, block), so
+    any sharding sees the same data. ragged=(lo, hi) draws C_b ~ U[lo, hi]; >= 1 click and >= 1
+    non-click per impression (reader.py:374)."""
+    his, masks, cands, sizes, labs = [], [], [], [], []
+    for j in range(start // BLOCK, (start + count + BLOCK - 1) // BLOCK):
+        g = torch.Generator(device="cpu").manual_seed(_mix(seed ^ 0x5EED, j))
+        n = BLOCK
+        hl = torch.randint(0, L + 1, (n,), generator=g)
+        ids = torch.randint(1, n_news, (n, L), generator=g)
+        m = torch.arange(L)[None, :] >= (L - hl)[:, None]
+        ids = torch.where(m, ids, torch.zeros_like(ids))
+        cnt = torch.randint(ragged[0], ragged[1] + 1, (n,), generator=g) if ragged else torch.full((n,), C)
+        N = int(cnt.sum())
+        cid = torch.randint(1, n_news, (N,), generator=g)
+        offs = torch.zeros(n + 1, dtype=torch.int64)
+        offs[1:] = torch.cumsum(cnt, 0)
+        lab = (torch.rand((N,), generator=g) < 0.2).to(torch.uint8)
+        pos_i = (torch.rand((n,), generator=g) * cnt).long().clamp_max(cnt - 1)
+        neg_i = (pos_i + 1 + (torch.rand((n,), generator=g) * (cnt - 1)).long()) % cnt
+        lab[offs[:-1] + pos_i] = 1
+        lab[offs[:-1] + neg_i] = 0
+        lo, hi = max(start - j * BLOCK, 0), min(start + count - j * BLOCK, BLOCK)
+        his.append(ids[lo:hi])
+        masks.append(m[lo:hi])
+        cands.append(cid[offs[lo]:offs[hi]])
+        labs.append(lab[offs[lo]:offs[hi]])
+        sizes.append(cnt[lo:hi])
+    cnt = torch.cat(sizes) if sizes else torch.zeros(0, dtype=torch.int64)
+    offs = torch.zeros(count + 1, dtype=torch.int32)
+    offs[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    dev = torch.device(device)
+    return Behaviors(torch.cat(his).to(dev, torch.int32), torch.cat(masks).to(dev), torch.cat(cands).to(dev, torch.int32),
+                     offs.to(dev), torch.cat(labs).to(dev), torch.arange(start, start + count, device=dev))
