@@ -12,6 +12,8 @@ B=32768
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
   echo "[gpu_profile] tests"
   timeout -k 10 900 python3 -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider > "$O/gpu_tests.log" 2>&1
+  timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, \"$R\"); import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
+  tail -1 "$O/smoke.log"
   tail -3 "$O/gpu_tests.log"
 fi
 echo "[gpu_profile] bench"
