@@ -720,44 +720,74 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           Frag<T> ring[PF1];
 #pragma unroll
           for (int s = 0; s < PF1; ++s) frag_load_tile(ring[s], w1t + min(s, ns - 1) * 1024, lane);
-          int j = 0;
+          if constexpr (kBf16) {
+            // the history fragments of slab s+1 are read from LDS before slab s's MFMAs: read right
+            // before use, every MFMA waited one LDS latency (lgkmcnt) — S1 was LDS-latency bound
+            Frag<T> c0, c1, n0, n1;
+            frag_load_E(c0, ldsE, l0, 0, h, rowB, g16);
+            frag_load_E(c1, ldsE, l1, 0, h, rowB, g16);
+            int j = 0;
 #pragma unroll
-          for (; j + PF1 <= ns; j += PF1) {
+            for (; j + PF1 <= ns; j += PF1) {
+#pragma unroll
+              for (int s = 0; s < PF1; ++s) {
+                if (j + s + 1 < ns) {
+                  frag_load_E(n0, ldsE, l0, (j + s + 1) * 32, h, rowB, g16);
+                  frag_load_E(n1, ldsE, l1, (j + s + 1) * 32, h, rowB, g16);
+                }
+                mma_slab<T>(acc0, ring[s], c0);
+                mma_slab<T>(acc1, ring[s], c1);
+                frag_load_tile(ring[s], w1t + min(j + s + PF1, ns - 1) * 1024, lane);
+                c0 = n0;
+                c1 = n1;
+                __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
+              }
+            }
 #pragma unroll
             for (int s = 0; s < PF1; ++s) {
-              const int kk = (j + s) * 32;
-              Frag<T> b0, b1;
-              if constexpr (kBf16) {
-                frag_load_E(b0, ldsE, l0, kk, h, rowB, g16);
-                frag_load_E(b1, ldsE, l1, kk, h, rowB, g16);
-              } else {
-                frag_load(b0, erow(l0) + kk + 16 * h);
-                frag_load(b1, erow(l1) + kk + 16 * h);
+              if (j + s < ns) {
+                if (j + s + 1 < ns) {
+                  frag_load_E(n0, ldsE, l0, (j + s + 1) * 32, h, rowB, g16);
+                  frag_load_E(n1, ldsE, l1, (j + s + 1) * 32, h, rowB, g16);
+                }
+                mma_slab<T>(acc0, ring[s], c0);
+                mma_slab<T>(acc1, ring[s], c1);
+                c0 = n0;
+                c1 = n1;
               }
-              mma_slab<T>(acc0, ring[s], b0);
-              mma_slab<T>(acc1, ring[s], b1);
-              frag_load_tile(ring[s], w1t + min(j + s + PF1, ns - 1) * 1024, lane);
-              __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
             }
-          }
+          } else {
+            int j = 0;
 #pragma unroll
-          for (int s = 0; s < PF1; ++s) {
-            if (j + s < ns) {
-              const int kk = (j + s) * 32;
-              Frag<T> b0, b1;
-              if constexpr (kBf16) {
-                frag_load_E(b0, ldsE, l0, kk, h, rowB, g16);
-                frag_load_E(b1, ldsE, l1, kk, h, rowB, g16);
-              } else {
+            for (; j + PF1 <= ns; j += PF1) {
+#pragma unroll
+              for (int s = 0; s < PF1; ++s) {
+                const int kk = (j + s) * 32;
+                Frag<T> b0, b1;
                 frag_load(b0, erow(l0) + kk + 16 * h);
                 frag_load(b1, erow(l1) + kk + 16 * h);
+                mma_slab<T>(acc0, ring[s], b0);
+                mma_slab<T>(acc1, ring[s], b1);
+                frag_load_tile(ring[s], w1t + min(j + s + PF1, ns - 1) * 1024, lane);
+                __builtin_amdgcn_sched_barrier(0);
               }
-              mma_slab<T>(acc0, ring[s], b0);
-              mma_slab<T>(acc1, ring[s], b1);
+            }
+#pragma unroll
+            for (int s = 0; s < PF1; ++s) {
+              if (j + s < ns) {
+                const int kk = (j + s) * 32;
+                Frag<T> b0, b1;
+                frag_load(b0, erow(l0) + kk + 16 * h);
+                frag_load(b1, erow(l1) + kk + 16 * h);
+                mma_slab<T>(acc0, ring[s], b0);
+                mma_slab<T>(acc1, ring[s], b1);
+              }
             }
           }
+          STAMP(10);
 #pragma unroll
           for (int e = 0; e < 16; ++e) { acc0[e] = act_tanh<T>(acc0[e]); acc1[e] = act_tanh<T>(acc1[e]); }
+          STAMP(11);
           // register e of lane (r, h) is c = 32*wave + 16h + e: 16 contiguous c of history row lr
           Frag<T> pf;
           if constexpr (kBf16) {

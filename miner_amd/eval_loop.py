@@ -10,6 +10,12 @@ impressions with ``ops.score_gather`` in large chunks, and the evaluation stays 
 
     python -m miner_amd.eval_loop --synthetic --num_impressions 20000            # 1 GPU
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m miner_amd.eval_loop --synthetic ...
+    python -m miner_amd.eval_loop --eval_behaviors_path behaviors.tsv --eval_news_path news.tsv \
+        --category2id_path category2id.json --news_table news_emb.npy --state_dict miner_state.pt
+
+(files: MIND tsv as the reference reads them; the news table is the news encoder's output, row 0 =
+the pad news, row 1+i = news.tsv line i; the state_dict is a reference Miner's, exported with
+torch.save(model.state_dict()) — see miner_amd/formats.py).
 """
 from __future__ import annotations
 
@@ -62,8 +68,13 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
 def main(argv=None):
     ap = argparse.ArgumentParser(description="MINER evaluation on MI355X (synthetic MIND-shaped data)",
                                  fromfile_prefix_chars="@", allow_abbrev=False)
-    ap.add_argument("--synthetic", action="store_true", required=True,
+    ap.add_argument("--synthetic", action="store_true",
                     help="synthetic impressions and random-init weights (no dataset or checkpoint here)")
+    ap.add_argument("--eval_behaviors_path")
+    ap.add_argument("--eval_news_path")
+    ap.add_argument("--category2id_path")
+    ap.add_argument("--news_table", help=".npy / .safetensors / weights-only .pt [n_news+1, d]")
+    ap.add_argument("--state_dict", help="reference Miner state_dict (torch.save(model.state_dict()))")
     ap.add_argument("--num_impressions", type=int, default=20000)
     ap.add_argument("--num_news", type=int, default=104_151, help="MIND-large has ~104k news")
     ap.add_argument("--his_length", type=int, default=50)
@@ -85,13 +96,34 @@ def main(argv=None):
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dt = torch.bfloat16 if args.precision == "bf16" else torch.float32
-    table = synthetic.news_table(args.seed, args.num_news, args.embed_dim, device=dev, dtype=dt)
-    W1, Q, W2 = synthetic.init_weights(args.seed, args.embed_dim, args.context_code_dim, args.num_context_codes,
-                                       device=dev)
+    if args.synthetic:
+        table = synthetic.news_table(args.seed, args.num_news, args.embed_dim, device=dev, dtype=dt)
+        W1, Q, W2 = synthetic.init_weights(args.seed, args.embed_dim, args.context_code_dim, args.num_context_codes,
+                                           device=dev)
+        start, count = distributed.shard_range(args.num_impressions, rank, world)
+        beh = synthetic.behaviors(args.seed, start, count, L=args.his_length, n_news=args.num_news,
+                                  C=args.candidates, ragged=args.ragged, device=dev)
+    else:
+        from . import formats
+        for a in ("eval_behaviors_path", "eval_news_path", "category2id_path", "news_table", "state_dict"):
+            if getattr(args, a) is None:
+                ap.error(f"--{a} is required without --synthetic")
+        news = formats.read_news_tsv(args.eval_news_path, formats.read_category2id(args.category2id_path))
+        table = formats.load_news_table(args.news_table).to(dev, dt)
+        if table.shape[0] != news.n_rows:
+            raise ValueError(f"news table has {table.shape[0]} rows, news.tsv + pad needs {news.n_rows}")
+        sd = torch.load(args.state_dict, map_location="cpu", weights_only=True)
+        W1, Q = sd["poly_attn.linear.weight"].to(dev), sd["poly_attn.context_codes"].to(dev)
+        W2 = sd["target_aware_attn.linear.weight"].to(dev) if args.score_type == "weighted" else None
+        every = formats.read_behaviors_tsv(args.eval_behaviors_path, news, args.his_length)
+        start, count = distributed.shard_range(every.n, rank, world)
+        o = every.cand_offsets
+        beh = synthetic.Behaviors(every.his_ids[start:start + count].to(dev), every.his_mask[start:start + count].to(dev),
+                                  every.cand_ids[int(o[start]):int(o[start + count])].to(dev),
+                                  (o[start:start + count + 1] - o[start]).to(dev),
+                                  every.labels[int(o[start]):int(o[start + count])].to(dev),
+                                  every.impression_ids[start:start + count].to(dev))
     packed = ops.pack_weights(W1, Q, W2 if args.score_type == "weighted" else None, dtype=dt)
-    start, count = distributed.shard_range(args.num_impressions, rank, world)
-    beh = synthetic.behaviors(args.seed, start, count, L=args.his_length, n_news=args.num_news, C=args.candidates,
-                              ragged=args.ragged, device=dev)
     # global sample offset of this shard (the eval loss's batch partition spans ranks)
     n_mine = torch.tensor([int(beh.cand_offsets[-1])], dtype=torch.float64)
     counts = distributed.all_gather_concat(n_mine.to(distributed._coll_device())).cpu().long().tolist()
@@ -104,8 +136,8 @@ def main(argv=None):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if rank == 0:
-        log.info("Model: Miner (MI355X fused scoring, %s); dataset: synthetic, %d impressions, %d samples, %d rank(s)",
-                 args.precision, args.num_impressions, total, world)
+        log.info("Model: Miner (MI355X fused scoring, %s); dataset: %s, %d samples, %d rank(s)",
+                 args.precision, "synthetic" if args.synthetic else args.eval_behaviors_path, total, world)
         log.info("----------------  Evaluation phrase  ----------------")
         if loss is not None:
             log.info("Loss %s", loss)

@@ -19,7 +19,9 @@ def pytest_configure(config):
 
 
 def golden_names():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    """The scoring fixtures (make_golden.py); reader_*.npz belong to the format tests."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
+                  if not os.path.basename(p).startswith("reader_"))
 
 
 def load_golden(name):
