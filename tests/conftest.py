@@ -19,9 +19,10 @@ def pytest_configure(config):
 
 
 def golden_names():
-    """The scoring fixtures (make_golden.py); reader_*.npz belong to the format tests."""
+    """The MINER scoring fixtures (make_golden.py); reader_*.npz belong to the format tests and
+    fastformer_*.npz to the FastFormer tests."""
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not os.path.basename(p).startswith("reader_"))
+                  if not os.path.basename(p).startswith(("reader_", "fastformer_")))
 
 
 def load_golden(name):

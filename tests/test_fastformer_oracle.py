@@ -1,0 +1,33 @@
+"""Pin the FastFormer oracle to the reference's own FastFormer (tests/golden/fastformer_*.npz). CPU."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fastformer_oracle as ffo
+from oracle import miner_oracle as orc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NAMES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(HERE, "golden", "fastformer_*.npz")))
+
+
+def load_ff(name):
+    z = np.load(os.path.join(HERE, "golden", name + ".npz"), allow_pickle=False)
+    g = {k: z[k] for k in z.files}
+    g["params"] = {k[2:]: torch.from_numpy(g[k]) for k in g if k.startswith("p.")}
+    g["E"] = g["table"][g["his_ids"]]
+    g["cand"] = g["table"][g["cand_ids"]]
+    return g
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_matches_reference(name):
+    g = load_ff(name)
+    E, M, Cd = torch.from_numpy(g["E"]), torch.from_numpy(g["his_mask"]), torch.from_numpy(g["cand"])
+    u = ffo.user_vectors(g["params"], E, M)
+    s = ffo.scores(g["params"], E, M, Cd)
+    assert np.array_equal(u.numpy(), g["user"]), "user vectors drifted from the reference op order"
+    assert np.array_equal(s.numpy(), g["scores"])
+    assert orc.parity_ok(s.numpy(), g["scores"])[0]

@@ -15,7 +15,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 STAMP_LIB = os.path.join(ROOT, "miner_amd", "libminer_hip_stamps.so")
-STAGES = ["S0 wait history DMA", "S1 W1·Eᵀ+tanh", "S2 Q·Pᵀ", "S3 softmax", "S4 A·E", "S5 W2+gelu", "S6 products", "S6 reduce", "S7 score", "loop tail"]
+STAGES = ["S0 wait history DMA", "S1 rest (S-partials+barrier)", "S2 Q·Pᵀ", "S3 softmax", "S4 A·E", "S5 W2+gelu",
+          "S6 products", "S6 reduce", "S7 score", "loop tail", "S1 loop (wave 0)", "S1 tanh (wave 0)"]
 
 
 
