@@ -31,6 +31,12 @@ SIGNATURES = {
     "miner_lds_bytes": (_I, [_I, _I, _I, _I, _I]),
     "miner_strerror": (ctypes.c_char_p, [_I]),
     "miner_abi_version": (_I, []),
+    # include/miner_fastformer.h
+    "miner_fastformer_packed_bytes": (ctypes.c_size_t, [_I]),
+    "miner_fastformer_pack": (_I, [_P, _I, _P, _P]),
+    "miner_fastformer_score": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "miner_fastformer_score_gather": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "miner_fastformer_lds_bytes": (_I, [_I]),
     # include/miner_metrics.h
     "miner_impression_metrics": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
 }

@@ -1,0 +1,235 @@
+// cdna4_common.h — device helpers shared by the HIP kernels of libminer_hip.so (gfx950 / CDNA4):
+// slab fragments and the 32x32 MFMA step over them, the pi row order of packed weight tiles,
+// DPP row reductions, bf16-mode transcendental approximations, LDS-DMA from inline asm.
+//
+// Slab layout (both dtypes): a "slab" is 32 consecutive contraction indices; lane l = 32h + r
+// (h = l>>5, r = l&31) holds 16 contiguous elements [16h, 16h+16) of row r of the slab. bf16: two
+// v_mfma_f32_32x32x16_bf16 steps (8 elements each); fp32: sixteen v_mfma_f32_32x32x2_f32 steps
+// (one element each, an exact fp32 fma chain). A 32x32 accumulator keeps row (e&3)+8(e>>2)+4h of
+// column r in register e; with the A-operand rows taken in the order pi(r) register e of lane half
+// h holds row 16h+e, so an accumulator IS a slab fragment of a following contraction over its rows.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+typedef __attribute__((address_space(3))) char lds_char;
+
+
+__host__ __device__ inline int pi_row(int r) { return 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3); }
+
+// ---------------------------------------------------------------------------------------------
+// element helpers
+// ---------------------------------------------------------------------------------------------
+template <class T> struct Frag;            // one lane's 16-element slab fragment
+template <> struct Frag<__bf16> { u32x4 q[2]; };
+template <> struct Frag<float> { u32x4 q[4]; };
+template <class T> constexpr int kNQ = sizeof(T);   // u32x4 per fragment (bf16: 2, fp32: 4)
+
+template <class T>
+__device__ __forceinline__ void frag_zero(Frag<T>& f) {
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = u32x4{0u, 0u, 0u, 0u};
+}
+
+// 16 contiguous elements from a 16-byte-aligned address (global or LDS)
+template <class T>
+__device__ __forceinline__ void frag_load(Frag<T>& f, const T* p) {
+  const u32x4* s = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = s[i];
+}
+
+// streamed-once data (candidate rows): non-temporal, so it does not evict the weights from L2
+#ifndef MINER_STREAM_NT
+#define MINER_STREAM_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void frag_load_stream(Frag<T>& f, const T* p) {
+  const u32x4* s = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = MINER_STREAM_NT ? __builtin_nontemporal_load(s + i) : s[i];
+}
+
+// slab fragment of a packed weight block (fragment-major, see the packed layout)
+template <class T>
+__device__ __forceinline__ void frag_load_tile(Frag<T>& f, const T* block, int lane) {
+  const u32x4* s = reinterpret_cast<const u32x4*>(block) + lane;
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) f.q[i] = s[64 * i];
+}
+
+template <class T>
+__device__ __forceinline__ void frag_store(T* p, const Frag<T>& f) {
+  u32x4* s = reinterpret_cast<u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i) s[i] = f.q[i];
+}
+
+template <class T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  __bf16 a = (__bf16)lo, b = (__bf16)hi;
+  return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+}
+
+// accumulator tile (rows taken in pi order) -> 16 contiguous elements / slab fragment
+template <class T>
+__device__ __forceinline__ void acc_to_frag(Frag<T>& f, const f32x16& x) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) f.q[m >> 2][m & 3] = pack_bf16x2(x[2 * m], x[2 * m + 1]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) f.q[e >> 2][e & 3] = __float_as_uint(x[e]);
+  }
+}
+
+// acc += A(slab) · B(slab) over 32 contraction indices
+template <class T>
+__device__ __forceinline__ void mma_slab(f32x16& acc, const Frag<T>& a, const Frag<T>& b) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a.q[s]),
+                                                    __builtin_bit_cast(bf16x8, b.q[s]), acc, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.q[t >> 2][t & 3]),
+                                                 __uint_as_float(b.q[t >> 2][t & 3]), acc, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
+
+// all-reduce over the 16 lanes of a DPP row: quad_perm xor1, xor2, row_half_mirror, row_mirror
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row16_max(float x) {
+  x = fmaxf(x, dpp_f<0xB1>(x));
+  x = fmaxf(x, dpp_f<0x4E>(x));
+  x = fmaxf(x, dpp_f<0x141>(x));
+  return fmaxf(x, dpp_f<0x140>(x));
+}
+__device__ __forceinline__ float row16_sum(float x) {
+  x += dpp_f<0xB1>(x);
+  x += dpp_f<0x4E>(x);
+  x += dpp_f<0x141>(x);
+  return x + dpp_f<0x140>(x);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) z[e] = 0.f;
+  return z;
+}
+
+// torch.nn.functional.gelu(approximate='none')
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+
+// bf16-mode transcendentals: branch-free, a handful of VALU ops each.  Their error (tanh: a few
+// fp32 ulp of 1; erf: <= 1.5e-7 absolute, Abramowitz & Stegun 7.1.26) is far below the bf16
+// operand rounding of that mode.  The fp32 parity mode uses the libm tanhf / erff / expf.
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(fminf(2.8853900817779268f * fabsf(x), 126.f));  // e^{2|x|}
+  return copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
+}
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float erfz = 1.0f - poly * __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z);
+  return 0.5f * x * (1.0f + copysignf(erfz, x));
+}
+// bf16-mode GELU without transcendentals, two values per packed-fp32 instruction (v_pk_fma_f32):
+// Φ(x) = 0.5 + x·P(x²) on |x| <= 4 (x clamped there), P the degree-7 weighted least-squares fit of
+// 0.5·erf(x/√2)/x: |ΔΦ| <= 5e-5, so |Δgelu(x)| <= 5e-5·|x| — far below bf16 operand rounding.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_poly2(f32x2 x) {
+  f32x2 xc;
+  xc.x = __builtin_amdgcn_fmed3f(x.x, -4.0f, 4.0f);
+  xc.y = __builtin_amdgcn_fmed3f(x.y, -4.0f, 4.0f);
+  const f32x2 u = xc * xc;
+  f32x2 q = f32x2{-1.5762298e-09f, -1.5762298e-09f};
+  q = __builtin_elementwise_fma(q, u, f32x2{1.2146164e-07f, 1.2146164e-07f});
+  q = __builtin_elementwise_fma(q, u, f32x2{-4.095486e-06f, -4.095486e-06f});
+  q = __builtin_elementwise_fma(q, u, f32x2{8.060949e-05f, 8.060949e-05f});
+  q = __builtin_elementwise_fma(q, u, f32x2{-0.0010478799f, -0.0010478799f});
+  q = __builtin_elementwise_fma(q, u, f32x2{0.0096639795f, 0.0096639795f});
+  q = __builtin_elementwise_fma(q, u, f32x2{-0.066174366f, -0.066174366f});
+  q = __builtin_elementwise_fma(q, u, f32x2{0.39884722f, 0.39884722f});
+  const f32x2 phi = __builtin_elementwise_fma(xc, q, f32x2{0.5f, 0.5f});
+  return x * phi;
+}
+// GELU over a whole accumulator tile: packed polynomial (bf16 mode) or exact erf (fp32 parity)
+template <class T>
+__device__ __forceinline__ void gelu_tile(f32x16& a) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      const f32x2 g = gelu_poly2(f32x2{a[e], a[e + 1]});
+      a[e] = g.x;
+      a[e + 1] = g.y;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) a[e] = gelu_erf(a[e]);
+  }
+}
+
+
+__device__ __forceinline__ unsigned lds_offset(const void* p) { return (unsigned)(uintptr_t)(const lds_char*)p; }
+
+// LDS-DMA from inline asm.  hipcc tracks its own global_load_lds and then waits vmcnt(0) before
+// every later LDS access it cannot prove disjoint; an asm DMA is invisible to that analysis.  Its
+// completion is the consumer's business: an explicit `s_waitcnt vmcnt(0)` before the barrier that
+// publishes the data (vm_wait_all).  hipcc's own vmcnt(N) waits stay correct — an older untracked
+// load only makes the in-order counter wait for one more.  M0 (the LDS base of the DMA) is saved
+// and restored around the instruction.  `lds` must be wave-uniform; lane i writes lds + i·size.
+__device__ __forceinline__ void dma_b128(const void* g, unsigned lds) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_b32(const void* g, unsigned lds) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Lane ids re-derived from an opaque copy of threadIdx.x at the top of every stage (see header).
+#define FRESH_LANE_IDS()                                              \
+  int tid_o_ = threadIdx.x;                                           \
+  asm volatile("" : "+v"(tid_o_));                                    \
+  const int tid = tid_o_;                                             \
+  const int lane = tid & 63;                                          \
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);          \
+  const int r = lane & 31;                                            \
+  const int h = lane >> 5;                                            \
+  (void)tid; (void)lane; (void)wave; (void)r; (void)h
+
+
+// element x (0..1023) of a fragment-major block -> (tile row rr, column cc)
+template <class T>
+__device__ __forceinline__ void block_pos(int x, int& rr, int& cc) {
+  constexpr int epp = 16 / (int)sizeof(T);      // elements per 16-byte piece
+  const int piece = x / epp, t = x % epp;
+  const int q = piece >> 6, l = piece & 63;     // piece q of lane l
+  rr = l & 31;
+  cc = 16 * (l >> 5) + q * epp + t;
+}
+
+}  // namespace

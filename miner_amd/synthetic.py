@@ -178,3 +178,22 @@ def behaviors(seed: int, start: int, count: int, *, L: int, n_news: int, C=40, r
     dev = torch.device(device)
     return Behaviors(torch.cat(his).to(dev, torch.int32), torch.cat(masks).to(dev), torch.cat(cands).to(dev, torch.int32),
                      offs.to(dev), torch.cat(labs).to(dev), torch.arange(start, start + count, device=dev))
+
+
+def fastformer_params(seed: int, device="cpu", affine_noise: bool = True) -> torch.Tensor:
+    """Random FastFormer user-encoder parameters as the flat fp32 blob of miner_fastformer_pack
+    (miner_amd.fastformer.PARAMS order). Weights ~ N(0, 0.02) as the reference's init
+    (model.py:497-509); with ``affine_noise`` the biases ~ N(0, 0.05) and LayerNorm gains
+    ~ 1 + N(0, 0.1) instead of the init's 0 / 1, so every parameter reaches the output."""
+    from .fastformer import PARAMS
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    parts = []
+    for name, shape in PARAMS:
+        if name.endswith("bias"):
+            t = torch.randn(shape, generator=g) * 0.05 if affine_noise else torch.zeros(shape)
+        elif "LayerNorm.weight" in name:
+            t = 1.0 + torch.randn(shape, generator=g) * 0.1 if affine_noise else torch.ones(shape)
+        else:
+            t = torch.randn(shape, generator=g) * 0.02
+        parts.append(t.reshape(-1))
+    return torch.cat(parts).to(device)

@@ -1,0 +1,190 @@
+"""FastFormer user-encoder kernel (miner_fastformer_score) — needs an MI355X.
+
+* fp32 parity mode vs the reference's own outputs (tests/golden/fastformer_*.npz, made by running
+  the reference FastFormer) and vs the oracle on random inputs: |x - ref| <= 1e-5|ref| + 1e-5·rms;
+* bf16 mode vs the oracle evaluated in fp32 on the SAME bf16-rounded inputs and weights:
+  |x - ref| <= 3e-2|ref| + 6e-2·rms (activations re-rounded to bf16 before each of the 13
+  matrix products, LayerNorms in between);
+* gather == dense and ragged == dense bit-exactly (same rows, deterministic kernel);
+* the drop-in modules load the reference state_dict and reproduce its scores.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from miner_amd import fastformer as ff
+from miner_amd import synthetic
+from oracle import fastformer_oracle as ffo
+from oracle import miner_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HERE = os.path.dirname(os.path.abspath(__file__))
+NAMES = ["cfg4_slice", "edge_short", "edge_empty", "edge_full"]
+BF16_TOL = dict(rtol=3e-2, rms_floor=6e-2)
+
+
+def load(name):
+    z = np.load(os.path.join(HERE, "golden", f"fastformer_{name}.npz"), allow_pickle=False)
+    g = {k: z[k] for k in z.files}
+    g["params"] = {k[2:]: torch.from_numpy(g[k]) for k in g if k.startswith("p.")}
+    return g
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def _oracle(params, E, M, Cd):
+    with torch.no_grad():
+        u = ffo.user_vectors(params, E.cpu().float(), M.cpu())
+        s = torch.matmul(Cd.cpu().float(), u.unsqueeze(-1)).squeeze(-1)
+    return s.numpy(), u.numpy()
+
+
+def _bf16_params(params):
+    """The bf16 kernel rounds the matrices to bf16 and keeps vectors / position embeddings fp32."""
+    out = {}
+    for k, v in params.items():
+        out[k] = _bf(v) if (v.dim() == 2 and "position_embeddings" not in k) else v
+    return out
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fp32_matches_reference(name):
+    g = load(name)
+    packed = ff.pack(ff.flatten_params(g["params"], DEV), torch.float32)
+    table = torch.from_numpy(g["table"]).to(DEV)
+    E, Cd = table[torch.from_numpy(g["his_ids"]).to(DEV)], table[torch.from_numpy(g["cand_ids"]).to(DEV)]
+    M = torch.from_numpy(g["his_mask"]).to(DEV)
+    s, u = ff.score(E, M, Cd, packed, return_user=True)
+    torch.cuda.synchronize()
+    ok_u, wu = orc.parity_ok(u.cpu().numpy(), g["user"])
+    ok_s, ws = orc.parity_ok(s.cpu().numpy(), g["scores"])
+    assert ok_u, f"user vectors off by {wu:.2f}x the fp32 bound"
+    assert ok_s, f"scores off by {ws:.2f}x the fp32 bound"
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_bf16_within_tolerance(name):
+    g = load(name)
+    packed = ff.pack(ff.flatten_params(g["params"], DEV), torch.bfloat16)
+    table = torch.from_numpy(g["table"])
+    E = _bf(table[torch.from_numpy(g["his_ids"])])
+    Cd = _bf(table[torch.from_numpy(g["cand_ids"])])
+    M = torch.from_numpy(g["his_mask"])
+    s = ff.score(E.to(DEV), M.to(DEV), Cd.to(DEV), packed)
+    ref, _ = _oracle(_bf16_params(g["params"]), E, M, Cd)
+    ok, worst = orc.parity_ok(s.cpu().numpy(), ref, **BF16_TOL)
+    assert ok, f"{name}: bf16 scores off by {worst:.2f}x the bf16 tolerance"
+
+
+def _random_case(seed, B, L, C, dtype, scale=0.0625, lens=None):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    n_news = 1 + B * (L + C)
+    table = torch.randn((n_news, 256), generator=g) * scale
+    his_ids = torch.randint(1, n_news, (B, L), generator=g)
+    if lens is None:
+        lens = torch.randint(0, L + 1, (B,), generator=g)
+    mask = torch.arange(L)[None, :] >= (L - lens)[:, None]
+    his_ids[~mask] = 0
+    cand_ids = torch.randint(1, n_news, (B, C), generator=g)
+    return table.to(dtype), his_ids, mask, cand_ids
+
+
+@pytest.mark.parametrize("L", [1, 17, 32, 33, 50, 64])
+def test_fp32_random_vs_oracle(L):
+    B, C = 37, 23
+    table, hid, mask, cid = _random_case(100 + L, B, L, C, torch.float32)
+    params = synthetic.fastformer_params(L)
+    pdict = {n: t for (n, _), t in zip(ff.PARAMS, torch.split(params, [int(np.prod(s)) for _, s in ff.PARAMS]))}
+    pdict = {n: pdict[n].reshape(s) for n, s in ff.PARAMS}
+    packed = ff.pack(params.to(DEV), torch.float32)
+    s, u = ff.score(table[hid].to(DEV), mask.to(DEV), table[cid].to(DEV), packed, return_user=True)
+    ref_s, ref_u = _oracle(pdict, table[hid], mask, table[cid])
+    ok_u, wu = orc.parity_ok(u.cpu().numpy(), ref_u)
+    ok_s, ws = orc.parity_ok(s.cpu().numpy(), ref_s)
+    assert ok_u and ok_s, (wu, ws)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gather_and_ragged_equal_dense(dtype):
+    B, L, C = 300, 50, 40
+    table, hid, mask, cid = _random_case(7, B, L, C, dtype)
+    packed = ff.pack(synthetic.fastformer_params(3).to(DEV), dtype)
+    table, hid, mask, cid = table.to(DEV), hid.to(DEV), mask.to(DEV), cid.to(DEV)
+    s_dense, u_dense = ff.score(table[hid], mask, table[cid], packed, return_user=True)
+    s_g, u_g = ff.score_gather(table, hid, mask, cid, packed, return_user=True)
+    assert torch.equal(s_dense, s_g) and torch.equal(u_dense, u_g)
+    # ragged: impression b keeps its first C_b candidates (C_b = 0 allowed)
+    sizes = torch.randint(0, C + 1, (B,), generator=torch.Generator().manual_seed(5))
+    sizes[3] = 0
+    offs = torch.zeros(B + 1, dtype=torch.int32)
+    offs[1:] = torch.cumsum(sizes, 0)
+    keep = (torch.arange(C)[None, :] < sizes[:, None]).to(DEV)
+    flat_ids = cid[keep]
+    s_r = ff.score(table[hid], mask, table[flat_ids], packed, cand_offsets=offs.to(DEV))
+    assert torch.equal(s_r, s_dense[keep])
+    s_rg = ff.score_gather(table, hid, mask, flat_ids, packed, cand_offsets=offs.to(DEV))
+    assert torch.equal(s_rg, s_dense[keep])
+    u_only = ff.score(table[hid], mask, None, packed)
+    assert torch.equal(u_only, u_dense)
+
+
+def test_large_batch_property():
+    """Config-4 sized launch (5000 impressions, more than one per workgroup): every impression's
+    scores equal the same impression scored alone in a small batch (no cross-impression state)."""
+    B, L, C = 5000, 50, 40
+    table, hid, mask, cid = _random_case(11, B, L, C, torch.bfloat16)
+    packed = ff.pack(synthetic.fastformer_params(4).to(DEV), torch.bfloat16)
+    table, hid, mask, cid = table.to(DEV), hid.to(DEV), mask.to(DEV), cid.to(DEV)
+    s = ff.score_gather(table, hid, mask, cid, packed)
+    idx = torch.tensor([0, 1, 255, 256, 2047, 4999], device=DEV)
+    s_small = ff.score_gather(table, hid[idx], mask[idx], cid[idx], packed)
+    assert torch.equal(s[idx], s_small)
+    assert torch.isfinite(s).all()
+
+
+def test_dropin_modules_reproduce_reference():
+    g = load("cfg4_slice")
+    table = torch.from_numpy(g["table"]).to(DEV)
+
+    class Stub(torch.nn.Module):
+        embed_dim = 256
+
+        def forward(self, title_encoding, title_attn_mask, sapo_encoding=None, sapo_attn_mask=None):
+            return table[title_encoding[:, 0]]
+
+    model = ff.FastFormer(news_encoder=Stub(), score_type="weighted", dropout=0.2).to(DEV).eval()
+    sd = {"fast_attn." + k: v for k, v in g["params"].items()}
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected and not [m for m in missing if m.startswith("fast_attn.")]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    title, his = t(g["cand_ids"])[..., None], t(g["his_ids"])[..., None]
+    ones = lambda x: torch.ones_like(x, dtype=torch.bool)
+    s = model(title=title, title_mask=ones(title), his_title=his, his_title_mask=ones(his),
+              his_mask=t(g["his_mask"]), sapo=title, sapo_mask=ones(title), his_sapo=his, his_sapo_mask=ones(his))
+    assert orc.parity_ok(s.cpu().numpy(), g["scores"])[0]
+    u = model.fast_attn(input_embs=table[t(g["his_ids"])], attention_mask=t(g["his_mask"]))
+    assert orc.parity_ok(u.cpu().numpy(), g["user"])[0]
+    # an in-place parameter update re-packs
+    with torch.no_grad():
+        model.fast_attn.encoders[1].output.LayerNorm.bias.add_(0.1)
+    u2 = model.fast_attn(input_embs=table[t(g["his_ids"])], attention_mask=t(g["his_mask"]))
+    p2 = dict(g["params"])
+    p2["encoders.1.output.LayerNorm.bias"] = p2["encoders.1.output.LayerNorm.bias"] + 0.1
+    ref_u2 = ffo.user_vectors(p2, torch.from_numpy(g["table"][g["his_ids"]]), torch.from_numpy(g["his_mask"]))
+    assert not orc.parity_ok(u2.cpu().numpy(), g["user"])[0]
+    assert orc.parity_ok(u2.cpu().numpy(), ref_u2.numpy())[0]
+    model.set_precision("bf16")
+    s_bf = model(title=title, title_mask=ones(title), his_title=his, his_title_mask=ones(his),
+                 his_mask=t(g["his_mask"]), sapo=title, sapo_mask=ones(title), his_sapo=his, his_sapo_mask=ones(his))
+    assert s_bf.dtype == torch.float32 and s_bf.shape == s.shape
+
+
+def test_cpu_tensors_raise():
+    packed = ff.pack(synthetic.fastformer_params(0).to(DEV), torch.float32)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ff.score(torch.zeros(2, 5, 256), torch.ones(2, 5, dtype=torch.bool), torch.zeros(2, 3, 256), packed)
