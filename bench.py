@@ -14,6 +14,10 @@ Also reported (same JSON line): the roofline of the dominant kernel (algorithmic
 launch over the HIP-event launch time, on the stream the kernel is launched on), the fp32 parity
 mode's throughput, and the CPU baseline (the oracle — a restatement of the reference's torch CPU
 path — timed on this host's cores over a bounded sample) on rank 0 at N=1.
+
+``--workload fastformer`` measures BASELINE config 4 instead (the FastFormer user encoder,
+SURVEY.md §8 f3): 50,000 impressions per GPU per step, history 50, 40 candidates, hidden 256,
+bf16, same JSON contract.
 """
 from __future__ import annotations
 
@@ -86,6 +90,148 @@ def cpu_baseline(seconds: float = 15.0):
                                     f"(reader.py:376-379 layout), {el2:.1f}s"}
 
 
+FF_L, FF_C, FF_H, FF_B = 50, 40, 256, 50000
+
+
+def ff_flops_per_impression(L=FF_L, C=FF_C, H=FF_H):
+    """Algorithmic FLOPs of the FastFormer user encoder + click predictor (model.py:345-545, :322):
+    per layer 6 H x H linears + 2 H -> 16 head projections + the 2 pooled attentions, then the
+    pooler (att_fc1, att_fc2, weighted sum) and C dot products; the MFMA pad of L to 64 excluded."""
+    layer = 6 * 2 * L * H * H + 2 * 2 * L * H * 16 + 2 * 2 * L * H
+    return 2 * layer + 2 * L * H * H + 2 * L * H + 2 * L * H + 2 * C * H
+
+
+def ff_bytes_per_impression(L=FF_L, C=FF_C, H=FF_H, elem=2):
+    """Algorithmic HBM bytes: history + candidate rows, mask, fp32 scores (parameters excluded)."""
+    return (L + C) * H * elem + L + 4 * C
+
+
+def ff_cpu_baseline(seconds: float = 15.0):
+    """FastFormer oracle (torch fp32 CPU restatement of model.py:345-545, :322) on host cores."""
+    from miner_amd import fastformer as ff
+    from miner_amd import synthetic
+    from oracle import fastformer_oracle as ffo
+    threads = torch.get_num_threads()
+    blob = synthetic.fastformer_params(0)
+    params = {n: t.reshape(shp) for (n, shp), t in
+              zip(ff.PARAMS, torch.split(blob, [int(torch.Size(shp).numel()) for _, shp in ff.PARAMS]))}
+    g = torch.Generator().manual_seed(1)
+    bs = 64
+    E = torch.randn(bs, FF_L, FF_H, generator=g) * 0.0625
+    M = torch.rand(bs, FF_L, generator=g) > 0.3
+    Cd = torch.randn(bs, FF_C, FF_H, generator=g) * 0.0625
+    with torch.no_grad():
+        ffo.scores(params, E, M, Cd)
+        pairs, t0, i = 0, time.perf_counter(), 0
+        while True:
+            ffo.scores(params, E, M, Cd)
+            pairs += bs * FF_C
+            i += 1
+            el = time.perf_counter() - t0
+            if el > seconds and i >= 2:
+                break
+    return {"value": round(pairs / el, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{pairs // FF_C} impressions x {FF_C} candidates (L={FF_L}, hidden {FF_H}), fp32, "
+                      f"batched {bs} impressions/call, {el:.1f}s"}
+
+
+def run_fastformer(args, rank, world, dev):
+    """BASELINE config 4: the FastFormer kernel over FF_B resident impressions per GPU per step."""
+    from miner_amd import fastformer as ff
+    from miner_amd import synthetic
+    B = args.batch if args.batch_set else FF_B
+    bf = torch.bfloat16
+    pool = []
+    for p in range(args.pool):
+        start = (rank * args.pool + p) * B
+        g = torch.Generator().manual_seed(1000 + start)
+        lens = torch.randint(0, FF_L + 1, (B,), generator=g)
+        mask = (torch.arange(FF_L)[None, :] >= (FF_L - lens)[:, None]).to(dev)
+        hist = (torch.randn(B, FF_L, FF_H, generator=g) * 0.0625).to(dev, bf)
+        cand = (torch.randn(B, FF_C, FF_H, generator=g) * 0.0625).to(dev, bf)
+        pool.append((hist, mask, cand))
+    blob = synthetic.fastformer_params(0).to(dev)
+    pk16 = ff.pack(blob, bf)
+    pk32 = ff.pack(blob, torch.float32)
+    torch.cuda.synchronize()
+
+    def step(i):
+        hist, mask, cand = pool[i % len(pool)]
+        return ff.score(hist, mask, cand, pk16)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        out = step(i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out).all()
+    f32 = None
+    if args.fp32_steps > 0:
+        hist, mask, cand = pool[0]
+        n32 = min(B, 5000)
+        h32, c32, m32 = hist[:n32].float(), cand[:n32].float(), mask[:n32]
+        ff.score(h32, m32, c32, pk32)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(args.fp32_steps):
+            ff.score(h32, m32, c32, pk32)
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms32 = a.elapsed_time(b) / args.fp32_steps
+        f32 = {"value": round(n32 * FF_C / (ms32 / 1e3), 1), "unit": "pairs/s", "ms_per_step": round(ms32, 3),
+               "impressions": n32,
+               "tflops": round(ff_flops_per_impression() * n32 / (ms32 / 1e3) / 1e12, 2)}
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    value = B * FF_C * args.steps * world / elapsed
+    fl = ff_flops_per_impression() * B
+    by = ff_bytes_per_impression() * B
+    tflops = fl / (kern_ms / 1e3) / 1e12
+    gbs = by / (kern_ms / 1e3) / 1e9
+    roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": "ff_fused<bf16>",
+            "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4)}
+    roof_hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_launch": by}
+    cpu = ff_cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
+    line = {
+        "metric": "(user,candidate) scores/sec, FastFormer user encoder (config 4)",
+        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (seeded config-4-shaped impressions, random-init weights)",
+        "config": {"workload": "config 4 FastFormer user encoder", "history": FF_L, "hidden": FF_H,
+                   "heads": 16, "layers": 2, "candidates": FF_C, "impressions_per_gpu_per_step": B,
+                   "global_batch": B * world,
+                   "parallelism": f"dp{world} (impression shards, no data-path collective)"},
+        "roofline": roof, "roofline_hbm": roof_hbm, "fp32_parity_mode": f32, "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def load_traffic(path):
     try:
         with open(path) as f:
@@ -102,13 +248,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32768, help="impressions per GPU per step")
+    ap.add_argument("--workload", default="config3", choices=["config3", "fastformer"])
+    ap.add_argument("--batch", type=int, default=None, help="impressions per GPU per step")
     ap.add_argument("--pool", type=int, default=2, help="distinct resident batches per GPU")
     ap.add_argument("--fp32-steps", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
+    args.batch_set = args.batch is not None
+    if args.batch is None:
+        args.batch = 32768
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -117,6 +267,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.workload == "fastformer":
+        return run_fastformer(args, rank, world, dev)
 
     from miner_amd import ops, synthetic
 
