@@ -42,7 +42,8 @@ extern "C" {
 
 #define MINER_ABI_VERSION 2
 
-enum miner_dtype { MINER_DTYPE_F32 = 0, MINER_DTYPE_BF16 = 1 };
+/* MINER_DTYPE_F16 is accepted by the full-corpus entry points of miner_corpus.h only (config 5) */
+enum miner_dtype { MINER_DTYPE_F32 = 0, MINER_DTYPE_BF16 = 1, MINER_DTYPE_F16 = 2 };
 
 /* src/model/model.py:128-136 ('weighted' = TargetAwareAttention). NONE = PolyAttention only. */
 enum miner_score_type {

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MINER_HIP_LIB", os.path.join(_HERE, "libminer_hip.so"))
 
 # enums of include/miner_score.h
-DTYPE_F32, DTYPE_BF16 = 0, 1
+DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
 SCORE_WEIGHTED, SCORE_MAX, SCORE_MEAN, SCORE_NONE = 0, 1, 2, 3
 SCORE_TYPES = {"weighted": SCORE_WEIGHTED, "max": SCORE_MAX, "mean": SCORE_MEAN, "none": SCORE_NONE}
 ABI_VERSION = 2
@@ -37,6 +37,11 @@ SIGNATURES = {
     "miner_fastformer_score": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "miner_fastformer_score_gather": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "miner_fastformer_lds_bytes": (_I, [_I]),
+    # include/miner_corpus.h
+    "miner_encoder_packed_bytes": (ctypes.c_size_t, [_I, _I, _I, _I]),
+    "miner_encoder_pack": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _P]),
+    "miner_encode_users": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "miner_rank_topk": (_I, [_P, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     # include/miner_metrics.h
     "miner_impression_metrics": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
 }

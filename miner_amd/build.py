@@ -15,8 +15,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "miner_score.hip")      # the fused scoring kernel
-SOURCES = [SRC, os.path.join(HERE, "csrc", "miner_metrics.hip"), os.path.join(HERE, "csrc", "fastformer.hip")]
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("miner_score.h", "miner_metrics.h", "miner_fastformer.h")] + [os.path.join(HERE, "csrc", "cdna4_common.h")]
+SOURCES = [SRC, os.path.join(HERE, "csrc", "miner_metrics.hip"), os.path.join(HERE, "csrc", "fastformer.hip"),
+           os.path.join(HERE, "csrc", "corpus.hip")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("miner_score.h", "miner_metrics.h", "miner_fastformer.h", "miner_corpus.h")] + [os.path.join(HERE, "csrc", "cdna4_common.h")]
 LIB = os.path.join(HERE, "libminer_hip.so")
 ARCH = os.environ.get("MINER_OFFLOAD_ARCH", "gfx950")
 

@@ -31,7 +31,10 @@ __host__ __device__ inline int pi_row(int r) { return 16 * ((r >> 2) & 1) + (r &
 // ---------------------------------------------------------------------------------------------
 template <class T> struct Frag;            // one lane's 16-element slab fragment
 template <> struct Frag<__bf16> { u32x4 q[2]; };
+template <> struct Frag<_Float16> { u32x4 q[2]; };
 template <> struct Frag<float> { u32x4 q[4]; };
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <class T> constexpr bool kIsF16 = __is_same(T, _Float16);
 template <class T> constexpr int kNQ = sizeof(T);   // u32x4 per fragment (bf16: 2, fp32: 4)
 
 template <class T>
@@ -76,6 +79,10 @@ __device__ __forceinline__ void frag_store(T* p, const Frag<T>& f) {
 
 template <class T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
 
+__device__ __forceinline__ unsigned pack_f16x2(float lo, float hi) {
+  _Float16 a = (_Float16)lo, b = (_Float16)hi;
+  return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+}
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
   __bf16 a = (__bf16)lo, b = (__bf16)hi;
   return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
@@ -84,7 +91,10 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
 // accumulator tile (rows taken in pi order) -> 16 contiguous elements / slab fragment
 template <class T>
 __device__ __forceinline__ void acc_to_frag(Frag<T>& f, const f32x16& x) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (kIsF16<T>) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) f.q[m >> 2][m & 3] = pack_f16x2(x[2 * m], x[2 * m + 1]);
+  } else if constexpr (sizeof(T) == 2) {
 #pragma unroll
     for (int m = 0; m < 8; ++m) f.q[m >> 2][m & 3] = pack_bf16x2(x[2 * m], x[2 * m + 1]);
   } else {
@@ -96,7 +106,12 @@ __device__ __forceinline__ void acc_to_frag(Frag<T>& f, const f32x16& x) {
 // acc += A(slab) · B(slab) over 32 contraction indices
 template <class T>
 __device__ __forceinline__ void mma_slab(f32x16& acc, const Frag<T>& a, const Frag<T>& b) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (kIsF16<T>) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a.q[s]),
+                                                   __builtin_bit_cast(f16x8, b.q[s]), acc, 0, 0, 0);
+  } else if constexpr (sizeof(T) == 2) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a.q[s]),
@@ -230,6 +245,19 @@ __device__ __forceinline__ void block_pos(int x, int& rr, int& cc) {
   const int q = piece >> 6, l = piece & 63;     // piece q of lane l
   rr = l & 31;
   cc = 16 * (l >> 5) + q * epp + t;
+}
+
+// history image in LDS (16-bit rows of a row-major matrix, one LDS-DMA 1 KiB block per wave-instruction)
+// Rows of 2d bytes packed back to back — the LDS-DMA (global_load_lds_dwordx4) writes each
+// wave's 1 KiB linearly — with 16-byte chunk c of row `row` stored at chunk c ^ eswz(row).  The
+// XOR is applied on the DMA's per-lane SOURCE address and again on every read: the 16 rows of a
+// ds_read_b128 lane group land in 16 different 16-byte slots (S1) and the 4 rows of a
+// ds_read_b64_tr_b16 block in 4 different 64-byte groups (S4), both conflict-free.
+// (g16: 16 chunks per 256 B) low 2 bits from the row's quad, (q + 2·(q>>2)) & 3, so that 16
+// consecutive rows AND 16 rows taken in pi order (quads 0,1,4,5 / 2,3,6,7: S1's operand rows) hit
+// 16 different slots
+__device__ __forceinline__ int eswz(int row, int g16) {
+  return g16 ? (((row & 3) << 2) | (((row >> 2) + ((row >> 4) << 1)) & 3)) : (((row & 1) << 2) | ((row >> 1) & 3));
 }
 
 }  // namespace

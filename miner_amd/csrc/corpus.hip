@@ -1,0 +1,814 @@
+// corpus.hip — full-corpus ranking for MI355X (gfx950 / CDNA4): BASELINE config 5, SURVEY.md §7
+// step 6 ("a users x news GEMM with fused softmax-over-K and a top-k epilogue; output never
+// materialised"). Two kernels:
+//
+//   ue_fused  user encoder, one workgroup (8 waves) per user, any L <= 256 and K <= 64:
+//             PolyAttention (model.py:159-185) -> mui [K,d] and proj = gelu(mui·W2ᵀ) (model.py:212)
+//     S1+S2  wave w owns history rows [32w, 32w+32): Pᵀ = tanh(W1·Eᵀ) for all 8 Dc-tiles (Dc padded
+//            to 256 with zero weights) and then Sᵀ = Q·Pᵀ straight from the accumulators — no
+//            cross-wave exchange; Sᵀ (+ bias) -> LDS
+//     S3     masked softmax over L per interest (masked logits = 1e-30, model.py:180)
+//     S4     muiᵀ = Eᵀ·Aᵀ over 32-row slabs of E LDS-DMA'd twice-buffered (16-bit: ds_read_b64_tr_b16
+//            Eᵀ fragments), wave w owning d-tiles w, w+8, ...
+//     S5     per interest tile: the mui image in LDS, projᵀ = gelu(W2·muiᵀ), W2 streamed (packed)
+//
+//   rk_fused  ranker: workgroup tile = 2 users x 256 news per step, contraction over d in 128-byte
+//             chunks staged through LDS by LDS-DMA (double buffered, XOR-swizzled rows); wave w owns
+//             user w>>2 and news [64(w&3), +64) and holds all of that user's K-row tiles (proj and
+//             mui) for its 64 news, so the click score (softmax over K of proj·e weighting mui·e,
+//             model.py:127-134, 213-214) is an in-register epilogue plus one lane-half exchange. Each
+//             workgroup owns whole users: a running top-k per user in LDS, threshold-filtered, so
+//             the U x N scores never leave the CU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "../../include/miner_corpus.h"
+#include "cdna4_common.h"
+
+namespace {
+
+constexpr int kThreads = 512;
+constexpr int kWaves = 8;
+constexpr int kMaxL = MINER_CORPUS_MAX_L;
+constexpr int kMaxK = MINER_CORPUS_MAX_K;
+constexpr int kMaxTopk = MINER_CORPUS_MAX_TOPK;
+constexpr int kDcT = 8;          // Dc padded to 8 tiles of 32
+constexpr int kMaxD = 768;
+
+inline bool aligned16(const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; }
+
+int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+
+__device__ __forceinline__ int fresh_lane() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t & 63;
+}
+
+template <class T> __device__ __forceinline__ float cx_exp(float x) {
+  if constexpr (sizeof(T) == 2) return __expf(x); else return expf(x);
+}
+template <class T> __device__ __forceinline__ float cx_tanh(float x) {
+  if constexpr (sizeof(T) == 2) return tanh_fast(x); else return tanhf(x);
+}
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+__device__ __forceinline__ float wave_max(float x) {
+  x = row16_max(x);
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return xor32_max(fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1])));
+}
+__device__ __forceinline__ float wave_sum(float x) {
+  x = row16_sum(x);
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return xor32_sum(__uint_as_float(s[0]) + __uint_as_float(s[1]));
+}
+
+// ================================================================================================
+// user encoder
+// ================================================================================================
+// packed weights (T elements): W1p [8 ct][ns] blocks (rows 32ct + pi(rr) of W1, zero past Dc),
+// Qp [nkt][8 c] blocks (rows 32kt + pi(rr) of Q, columns 32c.., zero past K / Dc),
+// W2p [ns][ns] blocks (rows 32jt + pi(rr) of W2); each block fragment-major (cdna4_common.h)
+__host__ __device__ inline size_t ue_w1_elems(int d) { return (size_t)kDcT * (d >> 5) * 1024; }
+__host__ __device__ inline size_t ue_q_elems(int K) { return (size_t)((K + 31) >> 5) * kDcT * 1024; }
+__host__ __device__ inline size_t ue_w2_elems(int d) { return (size_t)(d >> 5) * (d >> 5) * 1024; }
+
+template <class T>
+__global__ void ue_pack_kernel(const T* __restrict__ W1, const T* __restrict__ Q, const T* __restrict__ W2, int d,
+                               int Dc, int K, T* __restrict__ out) {
+  const size_t n1 = ue_w1_elems(d), nq = ue_q_elems(K), n2 = W2 ? ue_w2_elems(d) : 0;
+  const int ns = d >> 5;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n1 + nq + n2; i += (size_t)gridDim.x * blockDim.x) {
+    T v = (T)0.f;
+    int rr, cc;
+    block_pos<T>((int)(i & 1023), rr, cc);
+    if (i < n1) {
+      const int tile = (int)(i >> 10), ct = tile / ns, j = tile % ns;
+      const int row = 32 * ct + pi_row(rr);
+      if (row < Dc) v = W1[(size_t)row * d + 32 * j + cc];
+    } else if (i < n1 + nq) {
+      const int tile = (int)((i - n1) >> 10), kt = tile / kDcT, c = tile % kDcT;
+      const int row = 32 * kt + pi_row(rr), col = 32 * c + cc;
+      if (row < K && col < Dc) v = Q[(size_t)row * Dc + col];
+    } else {
+      const int tile = (int)((i - n1 - nq) >> 10), jt = tile / ns, j = tile % ns;
+      v = W2[(size_t)(32 * jt + pi_row(rr)) * d + 32 * j + cc];
+    }
+    out[i] = v;
+  }
+}
+
+struct UeParams {
+  const void* hist;        // dense [U, L, d], or the news table (gather)
+  const int32_t* his_ids;  // [U, L] or null
+  int n_news;
+  const uint8_t* mask;
+  const float* bias;
+  const void* wp;
+  float* mui_f32;          // [U, K, d] or null
+  void* user_mui;          // [U, K, d] T
+  void* user_proj;         // [U, K, d] T or null
+  int U, L, d, Dc, K;
+};
+
+// LDS carve (bytes)
+constexpr int kSS = kMaxL + 4;                          // S / fp32-A row stride (floats)
+constexpr int kSBytes = kMaxK * kSS * 4;                // logits; fp32 mode: A in place
+// mui image row stride (elements): an odd number of 16-byte units, so the 16 rows of a ds_read_b128
+// lane group land in 16 different bank slots
+template <class T> constexpr int kMS = kMaxD + 16 / (int)sizeof(T);
+template <class T> constexpr int kMuiImg = 32 * kMS<T> * (int)sizeof(T);  // one interest tile
+template <class T> constexpr int kEBuf = sizeof(T) == 2 ? 32 * kMaxD * 2 : 0;  // one E slab image (16-bit)
+template <class T> constexpr int kR1 = ((kSBytes > kMuiImg<T> ? kSBytes : kMuiImg<T>) > 2 * kEBuf<T>
+                                            ? (kSBytes > kMuiImg<T> ? kSBytes : kMuiImg<T>) : 2 * kEBuf<T>);
+constexpr int kAS = kMaxL + 8;                          // 16-bit A row stride (elements)
+template <class T> constexpr int kABytes = sizeof(T) == 2 ? kMaxK * kAS * 2 : 0;
+template <class T> constexpr int kOffA = kR1<T>;
+template <class T> constexpr int kOffIds = kOffA<T> + kABytes<T>;
+template <class T> constexpr int kOffZero = kOffIds<T> + kMaxL * 4;
+template <class T> constexpr int kUeLds = kOffZero<T> + 64;
+static_assert(kUeLds<__bf16> <= 160 * 1024 && kUeLds<float> <= 160 * 1024, "encoder LDS");
+
+// A-operand fragment of Eᵀ (rows = columns i0 + pi(..) of E, contraction over the 32 rows of an
+// E slab image) via ds_read_b64_tr_b16; rows >= nvalid read the zero block
+template <class T>
+__device__ __forceinline__ void frag_load_Et(Frag<T>& bf, unsigned img_off, unsigned zero_off, int i0, int rowB,
+                                             int g16, int nvalid, int lane) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int col = i0 + 16 * (pp & 1) + 8 * (g & 1) + 4 * (pp >> 1);
+  const int ch = col >> 3, sub8 = (col & 7) * 2;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = 16 * (g >> 1) + 8 * s + 4 * u + q;
+      const unsigned off = row < nvalid ? img_off + row * rowB + ((ch ^ eswz(row, g16)) << 4) + sub8 : zero_off;
+      const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)((lds_char*)smem + off));
+      bf.q[s][2 * u] = (unsigned)(unsigned short)v[0] | ((unsigned)(unsigned short)v[1] << 16);
+      bf.q[s][2 * u + 1] = (unsigned)(unsigned short)v[2] | ((unsigned)(unsigned short)v[3] << 16);
+    }
+  }
+}
+
+// nrows rows of d elements (dense from src, or table rows ids[r]) -> an E slab image (whole 1 KiB
+// DMA blocks; chunk c of row `row` at c ^ eswz(row))
+template <class T>
+__device__ __forceinline__ void ue_dma_slab(const T* src, const int32_t* idsL, int n_news, int nrows, int d,
+                                            char* img, int wave, int lane) {
+  const int cpr = d >> 3;
+  const int g16 = (cpr & 15) == 0;
+  const int total = nrows * cpr;
+  const int nblk = (total + 63) >> 6;
+  for (int blk = wave; blk < nblk; blk += kWaves) {
+    const int pos = blk * 64 + lane;
+    const int row = pos / cpr;
+    const int c = pos - row * cpr;
+    const int rr = min(row, nrows - 1);
+    const size_t r = idsL ? (size_t)min(max(idsL[rr], 0), n_news - 1) : (size_t)rr;
+    const T* g = (pos < total) ? src + r * d + (size_t)((c ^ eswz(row, g16)) << 3) : src;
+    dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
+  }
+}
+
+template <class T, int NKT, bool GATHER>
+__global__ __launch_bounds__(kThreads) void ue_fused(UeParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool k16 = sizeof(T) == 2;
+  const int L = p.L, d = p.d, K = p.K, ns = d >> 5;
+  const int nLt = (L + 31) >> 5;
+  const T* __restrict__ W1p = static_cast<const T*>(p.wp);
+  const T* __restrict__ Qp = W1p + ue_w1_elems(d);
+  const T* __restrict__ W2p = Qp + ue_q_elems(K);
+  float* S = reinterpret_cast<float*>(smem);
+  int32_t* idsL = reinterpret_cast<int32_t*>(smem + kOffIds<T>);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x < 16) reinterpret_cast<float*>(smem + kOffZero<T>)[threadIdx.x] = 0.f;
+
+  for (int u = blockIdx.x; u < p.U; u += gridDim.x) {
+    const T* __restrict__ base = static_cast<const T*>(p.hist) + (GATHER ? (size_t)0 : (size_t)u * L * d);
+    if constexpr (GATHER) {
+      __syncthreads();      // the previous user's readers of the id block are done
+      for (int i = threadIdx.x; i < L; i += kThreads) idsL[i] = p.his_ids[(size_t)u * L + i];
+    }
+    __syncthreads();
+
+    // ---- S1 + S2: wave w = history rows [32w, 32w + 32) ----
+    if (wave < nLt) {
+      const int lane = fresh_lane();
+      const int r = lane & 31, h = lane >> 5;
+      const int m = min(32 * wave + r, L - 1);
+      const T* erow = GATHER ? base + (size_t)min(max(idsL[m], 0), p.n_news - 1) * d : base + (size_t)m * d;
+      f32x16 acc[kDcT];
+#pragma unroll
+      for (int c = 0; c < kDcT; ++c) acc[c] = zero16();
+      for (int j = 0; j < ns; ++j) {
+        Frag<T> eb;
+        frag_load<T>(eb, erow + 32 * j + 16 * h);
+#pragma unroll
+        for (int c = 0; c < kDcT; ++c) {
+          Frag<T> wa;
+          frag_load_tile<T>(wa, W1p + (size_t)(c * ns + j) * 1024, lane);
+          mma_slab<T>(acc[c], wa, eb);          // Pᵀ[dc][l] over this d slab
+        }
+      }
+      f32x16 sacc[NKT];
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) sacc[kt] = zero16();
+#pragma unroll
+      for (int c = 0; c < kDcT; ++c) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[c][e] = cx_tanh<T>(acc[c][e]);     // model.py:171
+        Frag<T> pf;
+        acc_to_frag<T>(pf, acc[c]);            // lane (h, l): 16 consecutive Dc of row l
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+          Frag<T> qa;
+          frag_load_tile<T>(qa, Qp + (size_t)(kt * kDcT + c) * 1024, lane);
+          mma_slab<T>(sacc[kt], qa, pf);        // Sᵀ[k][l] (model.py:174)
+        }
+      }
+      const int l = 32 * wave + r;
+      const float bl = (p.bias && l < L) ? p.bias[(size_t)u * L + l] : 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) S[(32 * kt + 16 * h + e) * kSS + l] = sacc[kt][e] + bl;   // + bias (model.py:176)
+      }
+    }
+    __syncthreads();
+
+    // ---- S3: masked softmax over the history (model.py:178-181), 8 interests per wave ----
+    {
+      const int lane = fresh_lane();
+      const uint8_t* mrow = p.mask + (size_t)u * L;
+      bool real[kMaxL / 64];
+#pragma unroll
+      for (int i = 0; i < kMaxL / 64; ++i) {
+        const int l = lane + 64 * i;
+        real[i] = l < L && mrow[min(l, L - 1)] != 0;
+      }
+#pragma unroll
+      for (int q = 0; q < 32 * NKT / kWaves; ++q) {
+        const int k = wave * (32 * NKT / kWaves) + q;
+        float v[kMaxL / 64];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < kMaxL / 64; ++i) {
+          const int l = lane + 64 * i;
+          v[i] = l < L ? (real[i] ? S[k * kSS + l] : 1e-30f) : -INFINITY;
+          mx = fmaxf(mx, v[i]);
+        }
+        mx = wave_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < kMaxL / 64; ++i) {
+          v[i] = (lane + 64 * i < L) ? cx_exp<T>(v[i] - mx) : 0.f;
+          sum += v[i];
+        }
+        sum = wave_sum(sum);
+        const float inv = k < K ? 1.0f / sum : 0.f;
+#pragma unroll
+        for (int i = 0; i < kMaxL / 64; ++i) {
+          const int l = lane + 64 * i;
+          if constexpr (k16) reinterpret_cast<T*>(smem + kOffA<T>)[k * kAS + l] = (T)(v[i] * inv);
+          else S[k * kSS + l] = v[i] * inv;    // in place: this lane read exactly these entries
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- S4: muiᵀ = Eᵀ · Aᵀ, wave w owning d-tiles w, w + 8, ... ----
+    constexpr int kDt = kMaxD / 32 / kWaves;    // d-tiles per wave (<= 3)
+    f32x16 macc[kDt][NKT];
+#pragma unroll
+    for (int i = 0; i < kDt; ++i)
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) macc[i][kt] = zero16();
+    if constexpr (k16) {
+      const int rowB = 2 * d, g16 = (((d >> 3) & 15) == 0);
+      const int nls = nLt;
+      {
+        const int lane = fresh_lane();
+        ue_dma_slab<T>(base, GATHER ? idsL : nullptr, p.n_news, min(32, L), d, smem, wave, lane);
+      }
+      for (int s = 0; s < nls; ++s) {
+        vm_wait_all();
+        __syncthreads();      // slab s landed; slab s - 1's buffer is free
+        const int lane = fresh_lane();
+        const int r = lane & 31, h = lane >> 5;
+        if (s + 1 < nls) {
+          const int r0 = 32 * (s + 1);
+          ue_dma_slab<T>(GATHER ? base : base + (size_t)r0 * d, GATHER ? idsL + r0 : nullptr, p.n_news,
+                         min(32, L - r0), d, smem + ((s + 1) & 1) * kEBuf<T>, wave, lane);
+        }
+        const unsigned img = lds_offset(smem + (s & 1) * kEBuf<T>);
+        const unsigned zoff = lds_offset(smem + kOffZero<T>);
+        const int nvalid = min(32, L - 32 * s);
+        Frag<T> af[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+          frag_load<T>(af[kt], reinterpret_cast<const T*>(smem + kOffA<T>) + (32 * kt + r) * kAS + 32 * s + 16 * h);
+#pragma unroll
+        for (int i = 0; i < kDt; ++i) {
+          const int dt = wave + kWaves * i;
+          if (dt < ns) {
+            Frag<T> ef;
+            frag_load_Et<T>(ef, img, zoff, 32 * dt, rowB, g16, nvalid, lane);
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt) mma_slab<T>(macc[i][kt], ef, af[kt]);   // lane (h,k): d 16h..
+          }
+        }
+      }
+    } else {
+      // fp32 parity mode: E columns straight from L2 (one element per register), A rows natural
+      const int lane = fresh_lane();
+      const int r = lane & 31, h = lane >> 5;
+      for (int s = 0; s < nLt; ++s) {
+        Frag<T> af[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) frag_load<T>(af[kt], S + (32 * kt + r) * kSS + 32 * s + 16 * h);
+#pragma unroll
+        for (int i = 0; i < kDt; ++i) {
+          const int dt = wave + kWaves * i;
+          if (dt < ns) {
+            Frag<T> ef;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int l = min(32 * s + 16 * h + e, L - 1);      // rows >= L: finite x zero weight
+              const size_t row = GATHER ? (size_t)min(max(idsL[l], 0), p.n_news - 1) : (size_t)l;
+              ef.q[e >> 2][e & 3] = __float_as_uint(base[row * d + 32 * dt + r]);
+            }
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt) mma_slab<T>(macc[i][kt], af[kt], ef);   // lane (h,d): k rows
+          }
+        }
+      }
+    }
+    __syncthreads();          // E slab buffers / A free: the mui images go there
+
+    // ---- outputs: mui, then S5 per interest tile ----
+    {
+      const int lane = fresh_lane();
+      const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        T* img = reinterpret_cast<T*>(smem);         // [32 k][kMS]
+#pragma unroll
+        for (int i = 0; i < kDt; ++i) {
+          const int dt = wave + kWaves * i;
+          if (dt >= ns) continue;
+          if constexpr (k16) {
+            const int k = 32 * kt + r;
+            Frag<T> mf;
+            acc_to_frag<T>(mf, macc[i][kt]);
+            frag_store<T>(img + r * kMS<T> + 32 * dt + 16 * h, mf);
+            if (k < K) {
+              frag_store<T>(static_cast<T*>(p.user_mui) + ((size_t)u * K + k) * d + 32 * dt + 16 * h, mf);
+              if (p.mui_f32) {
+                float4* o = reinterpret_cast<float4*>(p.mui_f32 + ((size_t)u * K + k) * d + 32 * dt + 16 * h);
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                  o[g] = float4{macc[i][kt][4 * g], macc[i][kt][4 * g + 1], macc[i][kt][4 * g + 2], macc[i][kt][4 * g + 3]};
+              }
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int kl = acc_row(e, h), k = 32 * kt + kl;
+              img[kl * kMS<T> + 32 * dt + r] = macc[i][kt][e];
+              if (k < K) {
+                static_cast<T*>(p.user_mui)[((size_t)u * K + k) * d + 32 * dt + r] = macc[i][kt][e];
+                if (p.mui_f32) p.mui_f32[((size_t)u * K + k) * d + 32 * dt + r] = macc[i][kt][e];
+              }
+            }
+          }
+        }
+        if (p.user_proj) {
+          __syncthreads();    // the mui image of this interest tile is complete
+          // projᵀ = gelu(W2 · muiᵀ): wave w owns W2 row tiles w, w + 8, ...
+#pragma unroll
+          for (int i = 0; i < kDt; ++i) {
+            const int jt = wave + kWaves * i;
+            if (jt >= ns) continue;
+            f32x16 pacc = zero16();
+            for (int j = 0; j < ns; ++j) {
+              Frag<T> wa, mb;
+              frag_load_tile<T>(wa, W2p + (size_t)(jt * ns + j) * 1024, lane);
+              frag_load<T>(mb, img + r * kMS<T> + 32 * j + 16 * h);
+              mma_slab<T>(pacc, wa, mb);
+            }
+            gelu_tile<T>(pacc);                         // model.py:212 (exact erf in fp32 mode)
+            const int k = 32 * kt + r;
+            if (k < K) {
+              Frag<T> pf;
+              acc_to_frag<T>(pf, pacc);
+              frag_store<T>(static_cast<T*>(p.user_proj) + ((size_t)u * K + k) * d + 32 * jt + 16 * h, pf);
+            }
+          }
+        }
+        __syncthreads();      // before the next interest tile's image (or the next user) reuses LDS
+      }
+    }
+  }
+}
+
+// ================================================================================================
+// ranker
+// ================================================================================================
+constexpr int kUT = 2;            // users per workgroup tile
+constexpr int kNT = 256;          // news per step
+constexpr int kRowB = 128;        // bytes of every image row per d-chunk
+template <class T> constexpr int kEpc = kRowB / (int)sizeof(T);   // elements per chunk
+
+struct RkParams {
+  const void* mui;
+  const void* proj;
+  const void* news;
+  float* top_s;
+  int32_t* top_i;
+  int U, N, d, K, topk, score_type;
+};
+
+// image geometry: rows of 128 B, 16-byte chunk c of row `row` at c ^ ((row >> 1) & 7): the 16 rows
+// of a ds_read_b128 lane group (natural or pi order) hit 16 different slots
+__device__ __forceinline__ int rk_swz(int row) { return (row >> 1) & 7; }
+
+template <class T>
+__device__ __forceinline__ void rk_frag(Frag<T>& f, const char* img, int row, int c0) {
+#pragma unroll
+  for (int i = 0; i < kNQ<T>; ++i)
+    f.q[i] = *reinterpret_cast<const u32x4*>(img + row * kRowB + (((c0 + i) ^ rk_swz(row)) << 4));
+}
+
+// total order of ranked entries: higher score first, then lower news id
+__device__ __forceinline__ bool better(float s, int i, float s2, int i2) { return s > s2 || (s == s2 && i < i2); }
+
+template <int NR>
+struct RkLds {
+  static constexpr int kARows = kUT * NR * 32;
+  static constexpr int kStage = (kARows + kNT) * kRowB;
+  static constexpr int kOffList = 2 * kStage;                       // [kUT][kMaxTopk] float + int
+  static constexpr int kOffStage = kOffList + kUT * kMaxTopk * 8;  // staged candidates
+  static constexpr int kOffCnt = kOffStage + kUT * kNT * 8;         // list counts, staged counts
+  static constexpr int kTotal = kOffCnt + 64;
+};
+
+template <class T, int NKT, int SCORE>
+__global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool kW = SCORE == MINER_SCORE_WEIGHTED;
+  constexpr int NR = kW ? 2 * NKT : NKT;            // row tiles per user: mui (and proj)
+  using LD = RkLds<NR>;
+  constexpr int kChunkSlabs = sizeof(T) == 2 ? 2 : 1;
+  const int d = p.d, K = p.K, N = p.N;
+  const int nchunk = d * (int)sizeof(T) / kRowB;
+  const int nsteps = (N + kNT - 1) / kNT;
+  const int ntiles = (p.U + kUT - 1) / kUT;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int uu = wave >> 2, nsub = wave & 3;
+  float* list_s = reinterpret_cast<float*>(smem + LD::kOffList);
+  int* list_i = reinterpret_cast<int*>(smem + LD::kOffList + kUT * kMaxTopk * 4);
+  float* stg_s = reinterpret_cast<float*>(smem + LD::kOffStage);
+  int* stg_i = reinterpret_cast<int*>(smem + LD::kOffStage + kUT * kNT * 4);
+  int* cnt = reinterpret_cast<int*>(smem + LD::kOffCnt);           // [0,kUT): list sizes, [kUT, 2kUT): staged
+  const T* __restrict__ mui = static_cast<const T*>(p.mui);
+  const T* __restrict__ proj = static_cast<const T*>(p.proj);
+  const T* __restrict__ news = static_cast<const T*>(p.news);
+  const int first = blockIdx.x;
+  if (first >= ntiles) return;
+  const int ntile_mine = (ntiles - first + gridDim.x - 1) / gridDim.x;
+  const int total_chunks = ntile_mine * nsteps * nchunk;
+
+  // chunk sequence: (tile, step, chunk) -> DMA of its A rows (user k-rows) and B rows (news)
+  auto issue = [&](int q) {
+    const int lane = fresh_lane();
+    const int c = q % nchunk, st = (q / nchunk) % nsteps, ti = first + (q / nchunk / nsteps) * gridDim.x;
+    char* img = smem + (q & 1) * LD::kStage;
+    constexpr int kBlk = (LD::kARows + kNT) * kRowB / 1024;          // 1 KiB DMA blocks per stage
+    for (int blk = wave; blk < kBlk; blk += kWaves) {
+      const int P = blk * 64 + lane;
+      const int row = P >> 3, pc = P & 7;
+      const int cl = pc ^ rk_swz(row);
+      const T* g;
+      if (row < LD::kARows) {
+        const int ou = row / (NR * 32), t = (row / 32) % NR, rr = row % 32;
+        const int user = min(ti * kUT + ou, p.U - 1);
+        const int k = min(32 * (t % NKT) + rr, K - 1);
+        const T* src = (kW && t >= NKT) ? proj : mui;
+        g = src + ((size_t)user * K + k) * d + c * kEpc<T> + cl * (16 / (int)sizeof(T));
+      } else {
+        const int n = min(st * kNT + (row - LD::kARows), N - 1);
+        g = news + (size_t)n * d + c * kEpc<T> + cl * (16 / (int)sizeof(T));
+      }
+      dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
+    }
+  };
+
+  if (threadIdx.x < 2 * kUT) cnt[threadIdx.x] = 0;
+  issue(0);
+  int q = 0;
+  for (int ti = first; ti < ntiles; ti += gridDim.x) {
+    for (int st = 0; st < nsteps; ++st) {
+      f32x16 acc[NR][2];
+#pragma unroll
+      for (int t = 0; t < NR; ++t) { acc[t][0] = zero16(); acc[t][1] = zero16(); }
+      for (int c = 0; c < nchunk; ++c, ++q) {
+        vm_wait_all();
+        __syncthreads();        // chunk q landed; chunk q - 1's stage is free
+        if (q + 1 < total_chunks) issue(q + 1);
+        const int lane = fresh_lane();
+        const int r = lane & 31, h = lane >> 5;
+        const char* img = smem + (q & 1) * LD::kStage;
+        const char* bimg = img + LD::kARows * kRowB;
+#pragma unroll
+        for (int s = 0; s < kChunkSlabs; ++s) {
+          const int c0 = sizeof(T) == 2 ? 4 * s + 2 * h : 4 * h;
+          Frag<T> bf[2];
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) rk_frag<T>(bf[nt], bimg, 64 * nsub + 32 * nt + r, c0);
+#pragma unroll
+          for (int t = 0; t < NR; ++t) {
+            Frag<T> af;
+            rk_frag<T>(af, img, (uu * NR + t) * 32 + pi_row(r), c0);
+            mma_slab<T>(acc[t][0], af, bf[0]);
+            mma_slab<T>(acc[t][1], af, bf[1]);
+          }
+        }
+      }
+      // ---- epilogue: click score of (user uu, news) for this wave's 64 news ----
+      {
+        const int lane = fresh_lane();
+        const int r = lane & 31, h = lane >> 5;
+        const int user = ti * kUT + uu;
+        const float th_s = cnt[uu] < p.topk ? -INFINITY : list_s[uu * kMaxTopk + p.topk - 1];
+        const int th_i = cnt[uu] < p.topk ? 0x7fffffff : list_i[uu * kMaxTopk + p.topk - 1];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int n = st * kNT + 64 * nsub + 32 * nt + r;
+          float score;
+          if constexpr (kW) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (32 * kt + 16 * h + e < K) mx = fmaxf(mx, acc[NKT + kt][nt][e]);
+            mx = xor32_max(mx);
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (32 * kt + 16 * h + e < K) {
+                  const float ex = cx_exp<T>(acc[NKT + kt][nt][e] - mx);
+                  s0 += ex;
+                  s1 += ex * acc[kt][nt][e];
+                }
+            score = xor32_sum(s1) / xor32_sum(s0);       // Σ softmax_k(Lg) · M  (model.py:213-214)
+          } else if constexpr (SCORE == MINER_SCORE_MAX) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (32 * kt + 16 * h + e < K) mx = fmaxf(mx, acc[kt][nt][e]);
+            score = xor32_max(mx);                       // model.py:128-129
+          } else {
+            float sm = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (32 * kt + 16 * h + e < K) sm += acc[kt][nt][e];
+            score = xor32_sum(sm) / (float)K;            // model.py:130-131
+          }
+          const bool cand = h == 0 && n < N && user < p.U && better(score, n, th_s, th_i);
+          const unsigned long long bal = __ballot(cand);
+          if (bal) {
+            int b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&cnt[kUT + uu], __popcll(bal));
+            b0 = __builtin_amdgcn_readfirstlane(b0);
+            if (cand) {
+              const int slot = b0 + __popcll(bal & ((1ull << lane) - 1));
+              stg_s[uu * kNT + slot] = score;
+              stg_i[uu * kNT + slot] = n;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      // ---- merge the staged candidates into the running top-k (one wave per user) ----
+      if (nsub == 0) {
+        const int lane = fresh_lane();
+        const int ns_ = cnt[kUT + uu];
+        float* ls = list_s + uu * kMaxTopk;
+        int* li = list_i + uu * kMaxTopk;
+        int c = cnt[uu];
+        for (int j = 0; j < ns_; ++j) {
+          const float s = stg_s[uu * kNT + j];
+          const int id = stg_i[uu * kNT + j];
+          if (c == p.topk && !better(s, id, ls[p.topk - 1], li[p.topk - 1])) continue;
+          // insertion point: entries better than the candidate
+          int pos = 0;
+          float vs[kMaxTopk / 64];
+          int vi[kMaxTopk / 64];
+#pragma unroll
+          for (int t = 0; t < kMaxTopk / 64; ++t) {
+            const int i = lane + 64 * t;
+            vs[t] = ls[i];
+            vi[t] = li[i];
+            pos += __popcll(__ballot(i < c && better(vs[t], vi[t], s, id)));
+          }
+          // shift [pos, min(c, topk - 1)) up by one, then insert
+#pragma unroll
+          for (int t = 0; t < kMaxTopk / 64; ++t) {
+            const int i = lane + 64 * t;
+            if (i >= pos && i < c && i + 1 < p.topk) {
+              ls[i + 1] = vs[t];
+              li[i + 1] = vi[t];
+            }
+          }
+          if (lane == 0) {
+            ls[pos] = s;
+            li[pos] = id;
+          }
+          c = min(c + 1, p.topk);
+        }
+        if (lane == 0) {
+          cnt[uu] = c;
+          cnt[kUT + uu] = 0;
+        }
+      }
+      __syncthreads();
+    }
+    // ---- this tile's users are done: write their top-k ----
+    {
+      const int user = ti * kUT + uu;
+      if (nsub == 0 && user < p.U) {
+        const int lane = fresh_lane();
+        for (int i = lane; i < p.topk; i += 64) {
+          const bool ok = i < cnt[uu];
+          p.top_s[(size_t)user * p.topk + i] = ok ? list_s[uu * kMaxTopk + i] : -INFINITY;
+          p.top_i[(size_t)user * p.topk + i] = ok ? list_i[uu * kMaxTopk + i] : -1;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x < kUT) cnt[threadIdx.x] = 0;
+    }
+  }
+}
+
+// ================================================================================================
+// host side
+// ================================================================================================
+bool dtype_ok(int dt) { return dt == MINER_DTYPE_F32 || dt == MINER_DTYPE_BF16 || dt == MINER_DTYPE_F16; }
+size_t esize(int dt) { return dt == MINER_DTYPE_F32 ? 4 : 2; }
+
+template <class T, int NKT, bool G>
+int ue_launch(void* stream, const UeParams& prm) {
+  auto kern = ue_fused<T, NKT, G>;
+  const int lds = kUeLds<T>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return (int)e;
+  int grid = num_cus();
+  if (grid > prm.U) grid = prm.U;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+template <class T>
+int ue_dispatch(void* stream, const UeParams& prm) {
+  const bool g = prm.his_ids != nullptr;
+  if (prm.K <= 32) return g ? ue_launch<T, 1, true>(stream, prm) : ue_launch<T, 1, false>(stream, prm);
+  return g ? ue_launch<T, 2, true>(stream, prm) : ue_launch<T, 2, false>(stream, prm);
+}
+
+template <class T, int NKT, int S>
+int rk_launch(void* stream, const RkParams& prm) {
+  auto kern = rk_fused<T, NKT, S>;
+  constexpr int NR = S == MINER_SCORE_WEIGHTED ? 2 * NKT : NKT;
+  const int lds = RkLds<NR>::kTotal;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return (int)e;
+  const int ntiles = (prm.U + kUT - 1) / kUT;
+  int grid = num_cus();
+  if (grid > ntiles) grid = ntiles;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+template <class T>
+int rk_dispatch(void* stream, const RkParams& prm) {
+  const int st = prm.score_type;
+  if (prm.K <= 32) {
+    if (st == MINER_SCORE_WEIGHTED) return rk_launch<T, 1, MINER_SCORE_WEIGHTED>(stream, prm);
+    if (st == MINER_SCORE_MAX) return rk_launch<T, 1, MINER_SCORE_MAX>(stream, prm);
+    return rk_launch<T, 1, MINER_SCORE_MEAN>(stream, prm);
+  }
+  if (st == MINER_SCORE_WEIGHTED) return rk_launch<T, 2, MINER_SCORE_WEIGHTED>(stream, prm);
+  if (st == MINER_SCORE_MAX) return rk_launch<T, 2, MINER_SCORE_MAX>(stream, prm);
+  return rk_launch<T, 2, MINER_SCORE_MEAN>(stream, prm);
+}
+
+int check_dims(int dtype, int d, int Dc, int K) {
+  if (!dtype_ok(dtype) || d <= 0 || K <= 0 || Dc <= 0) return MINER_EINVAL;
+  if (K > kMaxK || Dc > 32 * kDcT || d > kMaxD) return MINER_ESHAPE;
+  if (d % (dtype == MINER_DTYPE_F32 ? 32 : 64)) return MINER_ESHAPE;
+  return MINER_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t miner_encoder_packed_bytes(int dtype, int d, int Dc, int K) {
+  if (check_dims(dtype, d, Dc, K) != MINER_OK) return 0;
+  return (ue_w1_elems(d) + ue_q_elems(K) + ue_w2_elems(d)) * esize(dtype);
+}
+
+int miner_encoder_pack(void* stream, int dtype, const void* w_poly, const void* context_codes, const void* w_target,
+                       int d, int Dc, int K, void* packed) {
+  const int ck = check_dims(dtype, d, Dc, K);
+  if (ck != MINER_OK) return ck;
+  if (!w_poly || !context_codes || !packed) return MINER_EINVAL;
+  if (!aligned16(packed)) return MINER_EALIGN;
+  const size_t n = ue_w1_elems(d) + ue_q_elems(K) + (w_target ? ue_w2_elems(d) : 0);
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dtype == MINER_DTYPE_BF16)
+    hipLaunchKernelGGL(ue_pack_kernel<__bf16>, dim3(grid), dim3(256), 0, s, static_cast<const __bf16*>(w_poly),
+                       static_cast<const __bf16*>(context_codes), static_cast<const __bf16*>(w_target), d, Dc, K,
+                       static_cast<__bf16*>(packed));
+  else if (dtype == MINER_DTYPE_F16)
+    hipLaunchKernelGGL(ue_pack_kernel<_Float16>, dim3(grid), dim3(256), 0, s, static_cast<const _Float16*>(w_poly),
+                       static_cast<const _Float16*>(context_codes), static_cast<const _Float16*>(w_target), d, Dc, K,
+                       static_cast<_Float16*>(packed));
+  else
+    hipLaunchKernelGGL(ue_pack_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<const float*>(w_poly),
+                       static_cast<const float*>(context_codes), static_cast<const float*>(w_target), d, Dc, K,
+                       static_cast<float*>(packed));
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+int miner_encode_users(void* stream, int dtype, const void* history, const int32_t* his_ids, int n_news,
+                       const uint8_t* his_mask, const float* his_bias, const void* packed, int U, int L, int d,
+                       int Dc, int K, float* mui_f32, void* user_mui, void* user_proj) {
+  const int ck = check_dims(dtype, d, Dc, K);
+  if (ck != MINER_OK) return ck;
+  if (U < 0 || L <= 0) return MINER_EINVAL;
+  if (L > kMaxL) return MINER_ESHAPE;
+  if (!history || !his_mask || !packed || !user_mui) return MINER_EINVAL;
+  if (his_ids && n_news <= 0) return MINER_EINVAL;
+  if (!aligned16(history) || !aligned16(packed) || !aligned16(user_mui) || !aligned16(user_proj) || !aligned16(mui_f32))
+    return MINER_EALIGN;
+  if (U == 0) return MINER_OK;
+  UeParams prm{};
+  prm.hist = history; prm.his_ids = his_ids; prm.n_news = n_news; prm.mask = his_mask; prm.bias = his_bias;
+  prm.wp = packed; prm.mui_f32 = mui_f32; prm.user_mui = user_mui; prm.user_proj = user_proj;
+  prm.U = U; prm.L = L; prm.d = d; prm.Dc = Dc; prm.K = K;
+  if (dtype == MINER_DTYPE_BF16) return ue_dispatch<__bf16>(stream, prm);
+  if (dtype == MINER_DTYPE_F16) return ue_dispatch<_Float16>(stream, prm);
+  return ue_dispatch<float>(stream, prm);
+}
+
+int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
+                    const void* news, int U, int N, int d, int K, int topk, float* top_scores, int32_t* top_ids) {
+  const int ck = check_dims(dtype, d, 1, K);
+  if (ck != MINER_OK) return ck;
+  if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_MEAN) return MINER_EINVAL;
+  if (U < 0 || N <= 0 || topk <= 0) return MINER_EINVAL;
+  if (topk > kMaxTopk) return MINER_ESHAPE;
+  if (!user_mui || !news || !top_scores || !top_ids) return MINER_EINVAL;
+  if (score_type == MINER_SCORE_WEIGHTED && !user_proj) return MINER_EINVAL;
+  if (!aligned16(user_mui) || !aligned16(user_proj) || !aligned16(news)) return MINER_EALIGN;
+  if (U == 0) return MINER_OK;
+  RkParams prm{};
+  prm.mui = user_mui; prm.proj = user_proj; prm.news = news; prm.top_s = top_scores; prm.top_i = top_ids;
+  prm.U = U; prm.N = N; prm.d = d; prm.K = K; prm.topk = topk; prm.score_type = score_type;
+  if (dtype == MINER_DTYPE_BF16) return rk_dispatch<__bf16>(stream, prm);
+  if (dtype == MINER_DTYPE_F16) return rk_dispatch<_Float16>(stream, prm);
+  return rk_dispatch<float>(stream, prm);
+}
+
+}  // extern "C"

@@ -122,17 +122,6 @@ template <class T> __device__ __forceinline__ float act_exp(float x) {
 // ---------------------------------------------------------------------------------------------
 // history image in LDS (bf16 mode)
 // ---------------------------------------------------------------------------------------------
-// Rows of 2d bytes packed back to back — the LDS-DMA (global_load_lds_dwordx4) writes each
-// wave's 1 KiB linearly — with 16-byte chunk c of row `row` stored at chunk c ^ eswz(row).  The
-// XOR is applied on the DMA's per-lane SOURCE address and again on every read: the 16 rows of a
-// ds_read_b128 lane group land in 16 different 16-byte slots (S1) and the 4 rows of a
-// ds_read_b64_tr_b16 block in 4 different 64-byte groups (S4), both conflict-free.
-// (g16: 16 chunks per 256 B) low 2 bits from the row's quad, (q + 2·(q>>2)) & 3, so that 16
-// consecutive rows AND 16 rows taken in pi order (quads 0,1,4,5 / 2,3,6,7: S1's operand rows) hit
-// 16 different slots
-__device__ __forceinline__ int eswz(int row, int g16) {
-  return g16 ? (((row & 3) << 2) | (((row >> 2) + ((row >> 4) << 1)) & 3)) : (((row & 1) << 2) | ((row >> 1) & 3));
-}
 
 // nrows rows of d elements -> the swizzled image (whole 1 KiB blocks, one per wave-instruction)
 // Gather mode: row r is table row ids[r] (ids in LDS), clamped to [0, n_news) so a bad id can

@@ -20,9 +20,9 @@ def pytest_configure(config):
 
 def golden_names():
     """The MINER scoring fixtures (make_golden.py); reader_*.npz belong to the format tests and
-    fastformer_*.npz to the FastFormer tests."""
+    fastformer_*.npz / corpus_*.npz to the FastFormer / full-corpus tests."""
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not os.path.basename(p).startswith(("reader_", "fastformer_")))
+                  if not os.path.basename(p).startswith(("reader_", "fastformer_", "corpus_")))
 
 
 def load_golden(name):

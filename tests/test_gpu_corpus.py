@@ -1,0 +1,128 @@
+"""Full-corpus ranking (BASELINE config 5; miner_encode_users + miner_rank_topk) — needs an MI355X.
+
+* fp32 parity mode vs the reference's own Miner scoring the whole table (tests/golden/corpus_*.npz):
+  mui within 1e-5·|ref| + 1e-5·rms; the returned top-k checked entry by entry against the
+  reference's score of that news id, best first, and no news outside the list beating the k-th;
+* 16-bit modes (bf16, fp16): the encoder vs the oracle on the same rounded inputs/weights
+  (3e-2·|ref| + 6e-2·rms), and the ranker vs the oracle evaluated on the kernel's own 16-bit user
+  vectors (only fp32 summation order differs: 2e-4·|ref| + 2e-4·rms);
+* gather == dense bit-exactly; odd U, N not a multiple of 256, topk > N, K = 32 and 64, L = 200.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from miner_amd import corpus
+from oracle import corpus_oracle as co
+from oracle import miner_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HERE = os.path.dirname(os.path.abspath(__file__))
+F32_TOL = dict(rtol=1e-5, rms_floor=1e-5)
+ENC16_TOL = dict(rtol=3e-2, rms_floor=6e-2)
+RANK16_TOL = dict(rtol=2e-4, rms_floor=2e-4)
+
+
+def load_corpus(name):
+    z = np.load(os.path.join(HERE, "golden", name + ".npz"), allow_pickle=False)
+    g = {k: z[k] for k in z.files}
+    g["score_type"] = str(g["score_type"])
+    return g
+
+
+def check_topk(ts, ti, ref_scores, k, tol):
+    """ts/ti: kernel top-k [U,k]; ref_scores [U,N] (float64 numpy)."""
+    ts, ti = ts.cpu().numpy().astype(np.float64), ti.cpu().numpy().astype(np.int64)
+    U, N = ref_scores.shape
+    rms = float(np.sqrt(np.mean(ref_scores ** 2)))
+    bound = lambda x: tol["rtol"] * np.abs(x) + tol["rms_floor"] * rms
+    for u in range(U):
+        n_ok = min(k, N)
+        assert (ti[u, n_ok:] == -1).all() and np.isneginf(ts[u, n_ok:]).all()
+        ids = ti[u, :n_ok]
+        assert len(set(ids.tolist())) == n_ok and (ids >= 0).all() and (ids < N).all()
+        true = ref_scores[u, ids]
+        assert (np.abs(ts[u, :n_ok] - true) <= bound(true)).all(), f"user {u}: returned scores off"
+        assert (np.diff(ts[u, :n_ok]) <= 0).all(), f"user {u}: not sorted"
+        kth = true.min()
+        rest = np.delete(ref_scores[u], ids)
+        assert (rest <= kth + 2 * bound(kth)).all(), f"user {u}: a news outside the top-k beats it"
+
+
+@pytest.mark.parametrize("name", ["corpus_c5_weighted", "corpus_c5_max", "corpus_k32_mean"])
+def test_fp32_matches_reference(name):
+    g = load_corpus(name)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    table, hid, mask = t(g["table"]), t(g["his_ids"]), t(g["his_mask"])
+    w2 = t(g["W2"]) if "W2" in g else None
+    pk = corpus.pack_encoder(t(g["W1"]), t(g["Q"]), w2, dtype=torch.float32)
+    mui, proj, m32 = corpus.encode_users(table[hid], mask, pk, with_proj=w2 is not None, return_f32=True)
+    assert orc.parity_ok(m32.cpu().numpy(), g["mui"], **F32_TOL)[0]
+    assert torch.equal(mui, m32)
+    mui_g, proj_g = corpus.encode_users(table, mask, pk, his_ids=hid, with_proj=w2 is not None)
+    assert torch.equal(mui_g, mui) and (proj is None or torch.equal(proj_g, proj))
+    N = table.shape[0]
+    for k in (17, 256):
+        ts, ti = corpus.rank_topk(mui, proj, table, k, score_type=g["score_type"])
+        check_topk(ts, ti, g["scores"].astype(np.float64), k, F32_TOL)
+
+
+def _round(x, dt):
+    return x.to(dt).to(torch.float32)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("score_type", ["weighted", "max"])
+def test_16bit_config5_dims(dtype, score_type):
+    """config-5 dimensions (L=200, K=64, d=768, Dc=200) on 33 users x 3000 news."""
+    gen = torch.Generator().manual_seed(5)
+    U, L, K, d, Dc, N = 33, 200, 64, 768, 200, 3000
+    table = torch.randn(N, d, generator=gen) / d ** 0.5
+    hl = torch.randint(0, L + 1, (U,), generator=gen)
+    mask = torch.arange(L)[None, :] >= (L - hl)[:, None]
+    hid = torch.where(mask, torch.randint(1, N, (U, L), generator=gen), torch.zeros(U, L, dtype=torch.long))
+    W1 = (torch.rand(Dc, d, generator=gen) * 2 - 1) / d ** 0.5
+    Q = (torch.rand(K, Dc, generator=gen) * 2 - 1) * 0.3
+    W2 = (torch.rand(d, d, generator=gen) * 2 - 1) / d ** 0.5
+    pk = corpus.pack_encoder(W1.to(DEV), Q.to(DEV), W2.to(DEV), dtype=dtype)
+    tab16 = table.to(DEV, dtype)
+    mui, proj = corpus.encode_users(tab16, mask.to(DEV), pk, his_ids=hid.to(DEV).int())
+    ref_mui, ref_proj = co.encode(_round(table, dtype)[hid], mask, _round(W1, dtype), _round(Q, dtype),
+                                  _round(W2, dtype))
+    assert orc.parity_ok(mui.float().cpu().numpy(), ref_mui.numpy(), **ENC16_TOL)[0]
+    assert orc.parity_ok(proj.float().cpu().numpy(), ref_proj.numpy(), **ENC16_TOL)[0]
+    ts, ti = corpus.rank_topk(mui, proj, tab16, 100, score_type=score_type)
+    ref = co.corpus_scores(mui.float().cpu(), proj.float().cpu(), _round(table, dtype), score_type)
+    check_topk(ts, ti, ref.double().numpy(), 100, RANK16_TOL)
+
+
+def test_topk_larger_than_table_and_k32():
+    gen = torch.Generator().manual_seed(9)
+    U, L, K, d, Dc, N = 5, 40, 32, 64, 96, 100
+    table = torch.randn(N, d, generator=gen) / d ** 0.5
+    mask = torch.ones(U, L, dtype=torch.bool)
+    hid = torch.randint(0, N, (U, L), generator=gen)
+    W1 = torch.randn(Dc, d, generator=gen) / d ** 0.5
+    Q = torch.randn(K, Dc, generator=gen) * 0.3
+    W2 = torch.randn(d, d, generator=gen) / d ** 0.5
+    pk = corpus.pack_encoder(W1.to(DEV), Q.to(DEV), W2.to(DEV), dtype=torch.float32)
+    mui, proj = corpus.encode_users(table.to(DEV)[hid.to(DEV)], mask.to(DEV), pk)
+    ref_mui, ref_proj = co.encode(table[hid], mask, W1, Q, W2)
+    assert orc.parity_ok(mui.cpu().numpy(), ref_mui.numpy(), **F32_TOL)[0]
+    for st in ("weighted", "max", "mean"):
+        ts, ti = corpus.rank_topk(mui, proj, table.to(DEV), 128, score_type=st)
+        ref = co.corpus_scores(ref_mui, ref_proj, table, st)
+        check_topk(ts, ti, ref.double().numpy(), 128, F32_TOL)
+
+
+def test_argument_errors():
+    z = torch.zeros(2, 64, 128, device=DEV)
+    with pytest.raises(ValueError):
+        corpus.rank_topk(z, z, torch.zeros(10, 128, device=DEV), 300)
+    with pytest.raises(ValueError):
+        corpus.rank_topk(z, z, torch.zeros(10, 128, device=DEV), 5, score_type="sum")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        corpus.rank_topk(z.cpu(), z.cpu(), torch.zeros(10, 128), 5)
