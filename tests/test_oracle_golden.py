@@ -24,10 +24,13 @@ def test_batched_scores_and_mui_match_reference(golden):
     g = golden
     mui, s = om.score_torch(_t(g["E"]), _t(g["his_mask"]), _t(g["cand"]), _t(g["W1"]), _t(g["Q"]),
                             _t(g["W2"]) if "W2" in g else None, g["score_type"], _bias(g))
-    # same ATen ops in the same order as model.py: expected bit-identical, gated at the §8c bar
+    # same ATen ops in the same order as model.py: bit-identical on the host that wrote the
+    # fixtures; on another host CPU (MKL/oneDNN kernel choice) the last bits move, so the pin is
+    # 20% of the §8c bar (which is also asserted).
     assert om.parity_ok(mui.numpy(), g["mui"])[0]
     assert om.parity_ok(s.numpy(), g["scores"])[0]
-    assert np.array_equal(s.numpy(), g["scores"]), "torch restatement drifted from the reference op order"
+    assert om.parity_ok(mui.numpy(), g["mui"], rtol=2e-6, rms_floor=2e-6)[0]
+    assert om.parity_ok(s.numpy(), g["scores"], rtol=2e-6, rms_floor=2e-6)[0], "torch restatement drifted"
 
 
 def test_per_candidate_layout_matches_reference(golden):
