@@ -42,6 +42,10 @@ SIGNATURES = {
     "miner_encoder_pack": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _P]),
     "miner_encode_users": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "miner_rank_topk": (_I, [_P, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    # include/miner_news.h
+    "miner_news_precompute": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _P]),
+    "miner_score_news": (_I, [_P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "miner_news_supported": (_I, [_I, _I, _I, _I, _I]),
     # include/miner_metrics.h
     "miner_impression_metrics": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
 }

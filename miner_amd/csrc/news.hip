@@ -1,0 +1,761 @@
+// news.hip — MINER scoring from news ids with a news-side precompute, MI355X
+// (gfx950 / CDNA4). Two kernels:
+//
+//   news_pre   per news row n of the table (one workgroup per 64 rows, 32 in fp32):
+//                logits[n] = tanh(W1·e_n)·Qᵀ       (model.py:171-174)           fp32 [n_news, K]
+//                proj[n]   = W2·e_n                 (model.py:212, pre-GELU)     T    [n_news, d]
+//              the rows of the tile are staged in LDS (LDS-DMA, XOR-swizzled), the packed weight
+//              tiles (miner_pack_weights) stream from L2 through a register ring: wave w owns the
+//              output column tiles w, w+8, ... of [W1 (Dc) | W2 (d)]; the W1 tiles go on through
+//              tanh and their Q contraction in registers, the per-tile logit partials are summed
+//              through LDS in a fixed order.
+//
+//   news_score per impression (one persistent workgroup of 8 waves per CU), from the history /
+//              candidate ids:
+//                A   = softmax_L(logits[his] + bias, masked slots = 1e-30)   (model.py:176-181)
+//                mui = A·E[his]                                              (model.py:182)
+//                X   = gelu(A·proj[his])  = gelu(mui·W2ᵀ)                    (model.py:212)
+//                M   = Cand·muiᵀ,  Lg = Cand·Xᵀ                              (model.py:127, :213)
+//                score = Σ_k softmax_k(Lg)·M  | max_k M | mean_k M           (model.py:128-136, :214)
+//              No weight is touched per impression: the kernel is a gather stream. The history rows
+//              of E and proj and the candidate rows are streamed in 64-column chunks through a ring
+//              of LDS slots (LDS-DMA by id, one 128-byte line per row per chunk in bf16), PD chunks
+//              in flight, one barrier per chunk. Per chunk wave w = (path P, slab sl, cand tile ct):
+//                P = 0:  muiᵀ[slab] = E[his]ᵀ·Aᵀ  (4 MFMA, E read transposed with
+//                        ds_read_b64_tr_b16), then M[ct] += Cand[ct]·muiᵀ[slab]
+//                P = 1:  Xᵀ[slab] = gelu(proj[his]ᵀ·Aᵀ), then Lg[ct] += Cand[ct]·Xᵀ[slab]
+//              The accumulator of a product is the operand of the next (rows taken in pi order, see
+//              cdna4_common.h): nothing but the rows themselves goes through LDS. The per-impression
+//              ids, mask, bias and logit rows ride in small LDS "aux" blocks, DMA'd one to three
+//              impressions ahead, so no load the compiler can see is ever waited on in the loop.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <stdio.h>
+
+#include "../../include/miner_news.h"
+#include "cdna4_common.h"
+
+namespace {
+
+constexpr int kThreads = 512;
+constexpr int kWaves = 8;
+constexpr int kMaxL = 64;
+constexpr int kMaxK = 32;
+constexpr int kMaxCand = MINER_NEWS_MAX_CAND;
+constexpr int kMaxD = 1024;
+constexpr int kMaxDc = 256;
+constexpr int kLdsMax = 160 * 1024;
+
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <class T> __device__ __forceinline__ float nx_exp(float x) {
+  if constexpr (sizeof(T) == 2) return __expf(x); else return expf(x);
+}
+template <class T> __device__ __forceinline__ float nx_tanh(float x) {
+  if constexpr (sizeof(T) == 2) return tanh_fast(x); else return tanhf(x);
+}
+
+// 32-lane (one half of the wave) all-reduce: DPP inside the 16-lane rows, then rows 0<->1, 2<->3
+__device__ __forceinline__ float half_max(float x) {
+  x = row16_max(x);
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  x = row16_sum(x);
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+// combine the two lane halves (permlane32_swap of x with itself: one result holds the low half's
+// value in every lane, the other the high half's)
+__device__ __forceinline__ float both_max(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+__device__ __forceinline__ float both_sum(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const char* p) { return *reinterpret_cast<const uint32_t*>(p); }
+__device__ __forceinline__ u32x4 lds_u32x4(const char* p) { return *reinterpret_cast<const u32x4*>(p); }
+
+// LDS-DMA of 16 bytes per lane with the default cache policy (table rows may be re-read by other
+// impressions: keep them in L2 / the Infinity Cache)
+__device__ __forceinline__ void dma_b128_c(const void* g, unsigned lds) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
+}
+#ifndef MINER_NEWS_NT
+#define MINER_NEWS_NT 0
+#endif
+__device__ __forceinline__ void dma_row(const void* g, unsigned lds) {
+  if constexpr (MINER_NEWS_NT) dma_b128(g, lds); else dma_b128_c(g, lds);
+}
+
+// ================================================================================================
+// per-news precompute
+// ================================================================================================
+// packed weight layout of miner_pack_weights (miner_score.hip): [W1p | Qp | W2p]
+__host__ __device__ inline int n_ct(int Dc) { return (Dc + 31) >> 5; }
+__host__ __device__ inline size_t w1p_el(int d, int Dc) { return (size_t)n_ct(Dc) * (d >> 5) * 1024; }
+__host__ __device__ inline size_t qp_el(int Dc) { return (size_t)n_ct(Dc) * 1024; }
+
+struct PreParams {
+  const void* table;
+  const void* wp;
+  float* logits;   // [N, K]
+  void* proj;      // [N, d] or null
+  int N, d, Dc, K;
+};
+
+template <class T> constexpr int kPreRows = sizeof(T) == 2 ? 64 : 32;   // news rows per tile
+
+// XOR swizzle of the 16-byte chunks of a tile row (cpr chunks per row, a multiple of 8): the 16
+// rows of a ds_read_b128 lane group land in 16 different bank slots
+__device__ __forceinline__ int pre_swz(int row, int cpr) { return (cpr & 15) ? (row & 7) : (row & 15); }
+
+template <class T, int NS>
+__global__ __launch_bounds__(kThreads) void news_pre(PreParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int R = kPreRows<T>;
+  constexpr int NRT = R / 32;
+  const int d = p.d;
+  const int ns = NS > 0 ? NS : (d >> 5);
+  const int nct = n_ct(p.Dc);
+  const int J = nct + (p.proj ? ns : 0);
+  const int rowB = d * (int)sizeof(T);
+  const int cpr = rowB >> 4;
+  const int imgB = R * rowB;
+  char* img = smem;
+  float* xch = reinterpret_cast<float*>(smem + imgB);     // [nct][NRT][16 regs][64 lanes]
+  const T* __restrict__ W1p = static_cast<const T*>(p.wp);
+  const T* __restrict__ Qp = W1p + w1p_el(d, p.Dc);
+  const T* __restrict__ W2p = Qp + qp_el(p.Dc);
+  const T* __restrict__ tab = static_cast<const T*>(p.table);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntiles = (p.N + R - 1) / R;
+  const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
+
+  auto issue_rows = [&](int tile) {
+    const int lane = threadIdx.x & 63;
+    const int n0 = tile * R;
+    for (int k = wave; k < (imgB >> 10); k += kWaves) {
+      const int o = (k << 10) + (lane << 4);
+      const int row = o / rowB;
+      const int piece = (o - row * rowB) >> 4;
+      const int n = min(n0 + row, p.N - 1);
+      const char* src = reinterpret_cast<const char*>(tab + (size_t)n * d) + ((piece ^ pre_swz(row, cpr)) << 4);
+      dma_b128(src, sbase + (k << 10));
+    }
+  };
+
+  int tile = blockIdx.x;
+  if (tile < ntiles) issue_rows(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int n0 = tile * R;
+    vm_wait_all();
+    raw_barrier();     // the tile's rows landed for every wave; last tile's partial readers done
+
+    for (int u = wave; u < J; u += kWaves) {
+      FRESH_LANE_IDS();
+      const bool w1 = u < nct;
+      const T* blk0 = w1 ? W1p + (size_t)u * ns * 1024 : W2p + (size_t)(u - nct) * ns * 1024;
+      f32x16 acc[NRT];
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt) acc[rt] = zero16();
+      auto step = [&](const Frag<T>& wf, int s) {
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+          const int row = 32 * rt + r;
+          const int ch = (32 * s + 16 * h) * (int)sizeof(T) / 16;   // first 16-byte chunk of columns [32s+16h, +16)
+          Frag<T> ef;
+#pragma unroll
+          for (int q = 0; q < kNQ<T>; ++q)
+            ef.q[q] = lds_u32x4(img + row * rowB + (((ch + q) ^ pre_swz(row, cpr)) << 4));
+          mma_slab(acc[rt], wf, ef);
+        }
+      };
+      if constexpr (NS > 0) {
+        constexpr int PF = NS < 4 ? NS : 4;
+        Frag<T> ring[PF];
+#pragma unroll
+        for (int s = 0; s < PF; ++s) frag_load_tile(ring[s], blk0 + (size_t)s * 1024, lane);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const Frag<T> wf = ring[s % PF];
+          if (s + PF < NS) frag_load_tile(ring[s % PF], blk0 + (size_t)(s + PF) * 1024, lane);
+          step(wf, s);
+        }
+      } else {
+        for (int s = 0; s < ns; ++s) {
+          Frag<T> wf;
+          frag_load_tile(wf, blk0 + (size_t)s * 1024, lane);
+          step(wf, s);
+        }
+      }
+      if (w1) {
+        // Sᵀ partial [k, news] = Q[:, tile u] · tanh(Pᵀ)[tile u, news]; Q rows in pi order
+        Frag<T> qf;
+        frag_load(qf, Qp + (size_t)pi_row(r) * (nct * 32) + 32 * u + 16 * h);
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[rt][e] = nx_tanh<T>(acc[rt][e]);
+          Frag<T> pf;
+          acc_to_frag<T>(pf, acc[rt]);
+          f32x16 sacc = zero16();
+          mma_slab(sacc, qf, pf);
+          float* dst = xch + ((size_t)(u * NRT + rt) * 16) * 64 + lane;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) dst[e * 64] = sacc[e];
+        }
+      } else {
+        const int jt = u - nct;
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+          const int n = n0 + 32 * rt + r;
+          if (n < p.N) {
+            Frag<T> of;
+            acc_to_frag<T>(of, acc[rt]);
+            frag_store(static_cast<T*>(p.proj) + (size_t)n * d + 32 * jt + 16 * h, of);
+          }
+        }
+      }
+    }
+    raw_barrier();     // partials written; the row image is free
+    if (tile + (int)gridDim.x < ntiles) issue_rows(tile + gridDim.x);
+    if (wave < NRT) {
+      FRESH_LANE_IDS();
+      const int n = n0 + 32 * wave + r;
+      float s[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s[e] = 0.f;
+      for (int u = 0; u < nct; ++u) {
+        const float* src = xch + ((size_t)(u * NRT + wave) * 16) * 64 + lane;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) s[e] += src[e * 64];
+      }
+      if (n < p.N) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          if (16 * h + e < p.K) p.logits[(size_t)n * p.K + 16 * h + e] = s[e];
+      }
+    }
+  }
+  vm_wait_all();
+}
+
+// ================================================================================================
+// per-impression scoring
+// ================================================================================================
+struct NsParams {
+  const void* table;
+  const float* logits;
+  const void* proj;
+  const int32_t* his_ids;
+  const uint8_t* mask;
+  const float* bias;
+  const int32_t* cand_ids;
+  const int32_t* cand_off;
+  float* scores;
+  float* mui_out;
+  int n_news, B, L, C, d, K, score_type;
+};
+
+#ifdef MINER_NEWS_DEBUG
+// diagnostic build only: every DMA / store address is range-checked, a violation is recorded in
+// g_news_dbg (kind bit, first offending value) and the access skipped
+__device__ unsigned long long g_news_dbg[4];
+__device__ __forceinline__ bool dbg_ok(int kind, const void* a, size_t n, const void* lo, size_t range, unsigned lds,
+                                       unsigned lds_n) {
+  const char* c = static_cast<const char*>(a);
+  const char* l = static_cast<const char*>(lo);
+  const bool ok = c >= l - 3 && c + n <= l + range && lds + lds_n <= (unsigned)(160 * 1024);
+  if (!ok) {
+    atomicOr(&g_news_dbg[0], 1ull << kind);
+    atomicCAS(&g_news_dbg[1 + (kind & 1)], 0ull, (unsigned long long)(c - l) + 1);
+    atomicCAS(&g_news_dbg[3], 0ull, (unsigned long long)lds + 1);
+  }
+  return ok;
+}
+#define NEWS_CHK(kind, a, n, lo, range, lds, lds_n) if (dbg_ok(kind, a, n, lo, range, lds, lds_n))
+#else
+#define NEWS_CHK(kind, a, n, lo, range, lds, lds_n)
+#endif
+
+template <class T> struct NCfg {
+  static constexpr int RB = 64 * (int)sizeof(T);     // bytes of one row of a 64-column chunk
+  static constexpr int PART = 64 * RB;               // 64 rows: E[his] | proj[his] | Cand
+  static constexpr int SLOT = 3 * PART;
+  static constexpr int NSLOT = sizeof(T) == 2 ? 4 : 2;
+  static constexpr int NI = RB / 128;                // DMA instructions per part per wave
+  static constexpr int RPI = 1024 / RB;              // rows per DMA instruction
+  static constexpr int PPR = RB / 16;                // 16-byte pieces per row
+};
+
+// LDS carve (bytes): [ring | xchg | logit blocks x2 | aux L1 x4 | aux L0 x4]
+constexpr int kRingB = 98304;                        // NSLOT * SLOT for both dtypes
+constexpr int kXchB = kWaves * 16 * 64 * 4;
+constexpr int kLogB = 64 * 128;                      // 64 history rows x K (<= 32) fp32
+constexpr int kL1B = 4 * 64 * 3 + 4 * kMaxCand;      // his ids | mask words | bias | cand ids
+constexpr int kL0B = 256;
+constexpr int kOffX = kRingB;
+constexpr int kOffLog = kOffX + kXchB;
+constexpr int kOffL1 = kOffLog + 2 * kLogB;
+constexpr int kOffL0 = kOffL1 + 4 * kL1B;
+constexpr int kNewsLds = kOffL0 + 4 * kL0B;
+static_assert(kNewsLds <= kLdsMax, "news_score LDS");
+static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>::NSLOT * NCfg<float>::SLOT == kRingB, "ring");
+
+// chunk swizzle of a slot row: bf16 (8 chunks per row, 2 rows per 256-byte bank row): rows 4q..4q+3
+// of a transposed read hit disjoint banks and 16 rows of a ds_read_b128 group distinct slots;
+// fp32 (16 chunks per row): row & 15
+template <class T> __device__ __forceinline__ int nswz(int row) {
+  if constexpr (sizeof(T) == 2) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+  else return row & 15;
+}
+
+// A-operand fragment of a part's transpose: rows = columns 32 sl + pi(r) of the chunk, contraction
+// over the 32 part rows 32 ls .. 32 ls + 31 (bf16: ds_read_b64_tr_b16)
+template <class T>
+__device__ __forceinline__ void load_partT(Frag<T>& f, const char* part, int ls, int sl, int lane) {
+  if constexpr (sizeof(T) == 2) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int col = 32 * sl + 16 * (pp & 1) + 8 * (g & 1) + 4 * (pp >> 1);
+    const int ch = col >> 3, sub = (col & 7) * 2;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int row = 32 * ls + 16 * (g >> 1) + 8 * s + 4 * u + q;
+        const char* a = part + row * 128 + ((ch ^ nswz<T>(row)) << 4) + sub;
+        const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds_char*)a);
+        f.q[s][2 * u] = (unsigned)(unsigned short)v[0] | ((unsigned)(unsigned short)v[1] << 16);
+        f.q[s][2 * u + 1] = (unsigned)(unsigned short)v[2] | ((unsigned)(unsigned short)v[3] << 16);
+      }
+    }
+  } else {
+    const int r = lane & 31, h = lane >> 5;
+    const int col = 32 * sl + pi_row(r);
+    const int ch = col >> 2, sub = (col & 3) * 4;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = 32 * ls + 16 * h + i;
+      f.q[i >> 2][i & 3] = lds_u32(part + row * 256 + ((ch ^ nswz<T>(row)) << 4) + sub);
+    }
+  }
+}
+
+// A-operand fragment of candidate rows 32 ct + pi(r), columns [32 sl + 16 h, +16) of the chunk
+template <class T>
+__device__ __forceinline__ void load_cand(Frag<T>& f, const char* part, int ct, int sl, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int row = 32 * ct + pi_row(r);
+  const int ch0 = sizeof(T) == 2 ? 4 * sl + 2 * h : 8 * sl + 4 * h;
+#pragma unroll
+  for (int q = 0; q < kNQ<T>; ++q)
+    f.q[q] = lds_u32x4(part + row * NCfg<T>::RB + (((ch0 + q) ^ nswz<T>(row)) << 4));
+}
+
+__device__ __forceinline__ int* l1_his(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B); }
+__device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return reinterpret_cast<uint32_t*>(smem + kOffL1 + slot * kL1B + 256); }
+__device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + kOffL1 + slot * kL1B + 512); }
+__device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B + 768); }
+__device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL0 + slot * kL0B); }
+
+template <class T>
+__global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using Cf = NCfg<T>;
+  const int G = gridDim.x;
+  const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
+  const int L = p.L, d = p.d, K = p.K;
+  const int nchunk = d >> 6;
+  const int PD = nchunk < Cf::NSLOT - 1 ? nchunk : Cf::NSLOT - 1;   // chunks in flight
+  const bool weighted = p.score_type == MINER_SCORE_WEIGHTED;
+  const bool ragged = p.cand_off != nullptr;
+  const bool with_cand = p.score_type != MINER_SCORE_NONE;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const T* __restrict__ tab = static_cast<const T*>(p.table);
+  const T* __restrict__ prj = p.proj ? static_cast<const T*>(p.proj) : tab;
+  const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
+
+  auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
+  // candidates of impression i (scores offset, count <= kMaxCand); L0 must have landed (ragged)
+  auto cands = [&](int i, int& off, int& cnt) {
+    if (!with_cand) { off = 0; cnt = 0; return; }
+    if (ragged) {
+      const int* o = l0_off(smem, i & 3);
+      off = __builtin_amdgcn_readfirstlane(o[0]);
+      cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
+    } else {
+      off = imp_b(i) * p.C;
+      cnt = p.C;
+    }
+    cnt = min(max(cnt, 0), kMaxCand);
+  };
+  auto npass_of = [&](int i) {
+    if (i >= n_i) return 1;
+    int off, cnt;
+    cands(i, off, cnt);
+    return max(1, (cnt + 63) >> 6);
+  };
+
+  // ---- aux DMA jobs (issued after a barrier, before that iteration's row DMAs) ----
+  auto issue_L0 = [&](int i) {           // CSR offsets of impression i
+    if (!ragged || i >= n_i || wave != 0) return;
+    const int lane = threadIdx.x & 63;
+    if (lane < 2) dma_b32(p.cand_off + imp_b(i) + lane, sbase + kOffL0 + (i & 3) * kL0B);
+  };
+  auto issue_L1 = [&](int i) {           // ids / mask / bias of impression i (needs L0(i))
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int b = imp_b(i);
+    const size_t base = (size_t)b * L + min(lane, L - 1);
+    if (wave == 1) {
+      NEWS_CHK(1, p.his_ids + base, 4, p.his_ids, (size_t)p.B * L * 4, sbase + kOffL1 + (i & 3) * kL1B, 256)
+      dma_b32(p.his_ids + base, sbase + kOffL1 + (i & 3) * kL1B);
+    } else if (wave == 2) {
+      // the aligned word holding mask byte `base` (the reader picks the byte by address)
+      const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
+      NEWS_CHK(2, reinterpret_cast<const void*>(a), 4, p.mask, (size_t)p.B * L + 3, sbase + kOffL1 + (i & 3) * kL1B + 256, 256)
+      dma_b32(reinterpret_cast<const void*>(a), sbase + kOffL1 + (i & 3) * kL1B + 256);
+    } else if (wave == 3) {
+      if (p.bias) dma_b32(p.bias + base, sbase + kOffL1 + (i & 3) * kL1B + 512);
+    } else if (wave >= 4 && with_cand) {   // waves 4..7: candidate ids, 64 per DMA
+      int off, cnt;
+      cands(i, off, cnt);
+      for (int j = wave - 4; 64 * j < cnt; j += 4) {
+        const int c = min(64 * j + lane, cnt - 1);
+        NEWS_CHK(3, p.cand_ids + off + c, 4, p.cand_ids, (size_t)(ragged ? 1 << 30 : p.B * p.C) * 4, sbase + kOffL1 + (i & 3) * kL1B + 768 + 256 * j, 256)
+        dma_b32(p.cand_ids + off + c, sbase + kOffL1 + (i & 3) * kL1B + 768 + 256 * j);
+      }
+    }
+  };
+  auto issue_L2 = [&](int i) {           // logit rows of impression i's history (needs L1(i))
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int row = min(8 * wave + (lane >> 3), L - 1);
+    const int piece = min(lane & 7, (K >> 2) - 1);
+    const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
+    NEWS_CHK(4, p.logits + (size_t)id * K + 4 * piece, 16, p.logits, (size_t)p.n_news * K * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
+    dma_b128_c(p.logits + (size_t)id * K + 4 * piece,
+               sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+  };
+  // rows of chunk `chunk` of pass `pass` of impression i -> ring slot `slot` (3 * NI DMAs per wave)
+  auto issue_rows = [&](int slot, int i, int pass, int chunk) {
+    const int lane = threadIdx.x & 63;
+    const bool live = i < n_i;
+    int off = 0, cnt = 1;
+    if (live) cands(i, off, cnt);
+    const int cntp = max(1, min(64, cnt - 64 * pass));
+    const int* hid = l1_his(smem, i & 3);
+    const int* cid = l1_cand(smem, i & 3);
+    const int piece = lane % Cf::PPR;
+#pragma unroll
+    for (int part = 0; part < 3; ++part) {
+#pragma unroll
+      for (int jj = 0; jj < Cf::NI; ++jj) {
+        const int blk = wave + 8 * jj;
+        const int rowp = blk * Cf::RPI + lane / Cf::PPR;
+        int id = 0;
+        if (live) id = part < 2 ? hid[min(rowp, L - 1)] : cid[min(64 * pass + min(rowp, cntp - 1), kMaxCand - 1)];
+        id = min(max(id, 0), p.n_news - 1);
+        const T* base = part == 1 ? prj : tab;
+        const char* src = reinterpret_cast<const char*>(base + (size_t)id * d + 64 * chunk) + ((piece ^ nswz<T>(rowp)) << 4);
+        NEWS_CHK(5 + part, src, 16, base, (size_t)p.n_news * d * sizeof(T), sbase + slot * Cf::SLOT + part * Cf::PART + blk * 1024, 1024)
+        dma_row(src, sbase + slot * Cf::SLOT + part * Cf::PART + blk * 1024);
+      }
+    }
+  };
+
+  // ---- prologue: aux for the first impressions, then the first PD chunks ----
+  issue_L0(0); issue_L0(1); issue_L0(2);
+  vm_wait_all();
+  raw_barrier();
+  issue_L1(0); issue_L1(1);
+  vm_wait_all();
+  raw_barrier();
+  issue_L2(0);
+  int qi = 0, qp = 0, qc = 0, qn = npass_of(0);   // issue cursor
+  for (int k = 0; k < PD; ++k) {
+    issue_rows(k, qi, qp, qc);
+    if (++qc == nchunk) { qc = 0; if (++qp == qn) { qp = 0; ++qi; qn = npass_of(qi); } }
+  }
+
+  Frag<T> af[2];                       // attention weights A [K, 64] as two B-operand slabs
+  f32x16 acc = zero16();               // this wave's M / Lg partial, one 32x32 candidate tile
+  const int P = wave >> 2, sl = (wave >> 1) & 1, ct = wave & 1;
+  bool pending = false;                // a finished pass waits for S7
+  int pend_off = 0, pend_cnt = 0;
+  int ci = 0, cp = 0, cc = 0, cn = npass_of(0);  // consumer cursor
+  int c_off = 0, c_cnt = 0;
+  int t = 0;
+
+  auto s7 = [&]() {
+    FRESH_LANE_IDS();
+    const int tct = wave & 1, e0 = 4 * (wave >> 1);
+    const float* X = reinterpret_cast<const float*>(smem + kOffX);
+    const bool kv = r < K;
+#pragma unroll
+    for (int ee = 0; ee < 4; ++ee) {
+      const int e = e0 + ee;
+      const float m = X[((0 + tct) * 16 + e) * 64 + lane] + X[((2 + tct) * 16 + e) * 64 + lane];
+      float sc;
+      if (p.score_type == MINER_SCORE_WEIGHTED) {
+        const float lg = X[((4 + tct) * 16 + e) * 64 + lane] + X[((6 + tct) * 16 + e) * 64 + lane];
+        const float mx = half_max(kv ? lg : -INFINITY);
+        const float pe = kv ? nx_exp<T>(lg - mx) : 0.f;
+        const float s = half_sum(pe);
+        const float num = half_sum(pe * m);
+        sc = num / s;
+      } else if (p.score_type == MINER_SCORE_MAX) {
+        sc = half_max(kv ? m : -INFINITY);
+      } else {
+        sc = half_sum(kv ? m : 0.f) / (float)K;
+      }
+      const int c = 32 * tct + 16 * h + e;
+      if (r == ee && c < pend_cnt) {
+        NEWS_CHK(8, p.scores + pend_off + c, 4, p.scores, (size_t)(ragged ? 1 << 30 : p.B * p.C) * 4, 0, 0)
+        p.scores[pend_off + c] = sc;
+      }
+    }
+  };
+
+  while (ci < n_i) {
+    // slot t landed (this wave's DMAs: all but the PD-1 younger chunks), then for every wave
+    if (PD >= 3) vm_wait<3 * Cf::NI * 2>(); else if (PD == 2) vm_wait<3 * Cf::NI>(); else vm_wait<0>();
+    raw_barrier();
+    const bool first = cp == 0 && cc == 0;
+    if (first) {
+      issue_L0(ci + 3);
+      issue_L1(ci + 2);
+      issue_L2(ci + 1);
+    }
+    const bool did_s7 = pending && with_cand;
+    if (did_s7) s7();
+    pending = false;
+    issue_rows((t + PD) % Cf::NSLOT, qi, qp, qc);
+    if (++qc == nchunk) { qc = 0; if (++qp == qn) { qp = 0; ++qi; qn = npass_of(qi); } }
+
+    if (first) {
+      // ---- attention weights of impression ci: softmax over the history (model.py:176-181) ----
+      FRESH_LANE_IDS();
+      const int b = imp_b(ci);
+      const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (ci & 1) * kLogB);
+      const uint32_t* mw = l1_mask(smem, ci & 3);
+      const float* bs = l1_bias(smem, ci & 3);
+      float v[32];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const int l = 32 * (j >> 4) + 16 * h + (j & 15);
+        float s = -INFINITY;
+        if (l < L) {
+          s = lgb[l * 32 + r];
+          if (p.bias) s += bs[l];
+          const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)b * L + l) & 3);
+          if (((mw[l] >> (8 * a)) & 0xffu) == 0u) s = 1e-30f;      // masked_fill_(~mask, 1e-30)
+        }
+        v[j] = s;
+        mx = fmaxf(mx, s);
+      }
+      mx = both_max(mx);
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const int l = 32 * (j >> 4) + 16 * h + (j & 15);
+        v[j] = l < L ? nx_exp<T>(v[j] - mx) : 0.f;
+        sum += v[j];
+      }
+      sum = both_sum(sum);
+      const float inv = r < K ? 1.0f / sum : 0.f;
+#pragma unroll
+      for (int ls = 0; ls < 2; ++ls) {
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int m = 0; m < 8; ++m) af[ls].q[m >> 2][m & 3] = pack_bf16x2(v[16 * ls + 2 * m] * inv, v[16 * ls + 2 * m + 1] * inv);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) af[ls].q[e >> 2][e & 3] = __float_as_uint(v[16 * ls + e] * inv);
+        }
+      }
+    }
+    if (cc == 0) {
+      acc = zero16();
+      cands(ci, c_off, c_cnt);
+    }
+    const int cntp = min(64, c_cnt - 64 * cp);
+
+    // ---- this chunk: X / mui slab, then the candidate product ----
+    const bool need_x = (P == 0) ? (with_cand || (p.mui_out && cp == 0)) : weighted;
+    const bool need_c = with_cand && (ct == 0 || cntp > 32) && (P == 0 || weighted);
+    const bool need_mui = P == 0 && p.mui_out && cp == 0 && ct == 0;
+    if (need_x && (need_c || need_mui)) {
+      FRESH_LANE_IDS();
+      const char* slot = smem + (t % Cf::NSLOT) * Cf::SLOT;
+      f32x16 ax = zero16();
+#pragma unroll
+      for (int ls = 0; ls < 2; ++ls) {
+        Frag<T> ef;
+        load_partT<T>(ef, slot + P * Cf::PART, ls, sl, lane);
+        mma_slab(ax, ef, af[ls]);
+      }
+      if (need_mui && r < K) {
+        float* dst = p.mui_out + ((size_t)imp_b(ci) * K + r) * d + 64 * cc + 32 * sl + 16 * h;
+#pragma unroll
+        for (int e = 0; e < 16; e += 4) *reinterpret_cast<float4*>(dst + e) = make_float4(ax[e], ax[e + 1], ax[e + 2], ax[e + 3]);
+      }
+      if (need_c) {
+        if (P == 1) gelu_tile<T>(ax);
+        Frag<T> xf, cf;
+        acc_to_frag<T>(xf, ax);
+        load_cand<T>(cf, slot + 2 * Cf::PART, ct, sl, lane);
+        mma_slab(acc, cf, xf);
+      }
+    }
+
+    if (cc == nchunk - 1) {            // pass done: partials -> LDS, S7 next iteration
+      if (nchunk == 1 && did_s7) raw_barrier();
+      const int lane = threadIdx.x & 63;
+      float* dst = reinterpret_cast<float*>(smem + kOffX) + (wave * 16) * 64 + lane;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dst[e * 64] = acc[e];
+      pending = true;
+      pend_off = c_off + 64 * cp;
+      pend_cnt = cntp;
+    }
+    ++t;
+    if (++cc == nchunk) { cc = 0; if (++cp == cn) { cp = 0; ++ci; cn = npass_of(ci); } }
+  }
+  vm_wait_all();
+  raw_barrier();
+  if (pending && with_cand) s7();
+}
+
+// ================================================================================================
+// host side
+// ================================================================================================
+int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+
+inline bool aligned16(const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; }
+
+int check_news(int dtype, int L, int d, int Dc, int K) {
+  if (dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) return MINER_EINVAL;
+  if (L <= 0 || d <= 0 || K <= 0 || Dc <= 0) return MINER_EINVAL;
+  if (L > kMaxL || K > kMaxK || (K & 3) || d % 64 || d > kMaxD || Dc > kMaxDc) return MINER_ESHAPE;
+  return MINER_OK;
+}
+
+int pre_lds(int dtype, int d, int Dc) {
+  const int es = dtype == MINER_DTYPE_BF16 ? 2 : 4;
+  const int R = dtype == MINER_DTYPE_BF16 ? 64 : 32;
+  return R * d * es + n_ct(Dc) * (R / 32) * 16 * 64 * 4;
+}
+
+template <class T, int NS>
+int launch_pre(void* stream, const PreParams& prm, int lds) {
+  auto kern = news_pre<T, NS>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return (int)e;
+  const int R = kPreRows<T>;
+  int grid = (prm.N + R - 1) / R;
+  if (grid > num_cus()) grid = num_cus();
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+template <class T>
+int run_pre(void* stream, const PreParams& prm, int lds) {
+  switch (prm.d >> 5) {
+    case 2: return launch_pre<T, 2>(stream, prm, lds);
+    case 4: return launch_pre<T, 4>(stream, prm, lds);
+    case 8: return launch_pre<T, 8>(stream, prm, lds);
+    case 16: return launch_pre<T, 16>(stream, prm, lds);
+    case 24: return launch_pre<T, 24>(stream, prm, lds);
+    default: return launch_pre<T, 0>(stream, prm, lds);
+  }
+}
+
+template <class T>
+int launch_score(void* stream, const NsParams& prm) {
+  auto kern = news_score<T>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kNewsLds);
+  if (e != hipSuccess) return (int)e;
+  int grid = num_cus();
+  if (grid > prm.B) grid = prm.B;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), kNewsLds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+#ifdef MINER_NEWS_DEBUG
+  unsigned long long h[4] = {0, 0, 0, 0};
+  hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  hipMemcpyFromSymbol(h, HIP_SYMBOL(g_news_dbg), sizeof(h));
+  fprintf(stderr, "[news_score debug] kinds=0x%llx off_odd=%lld off_even=%lld lds=%lld\n", h[0], (long long)h[1] - 1,
+          (long long)h[2] - 1, (long long)h[3] - 1);
+  unsigned long long z[4] = {0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_news_dbg), z, sizeof(z));
+#endif
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int miner_news_supported(int dtype, int L, int d, int Dc, int K) {
+  const int rc = check_news(dtype, L, d, Dc, K);
+  if (rc != MINER_OK) return rc;
+  return pre_lds(dtype, d, Dc) > kLdsMax ? MINER_ELDS : MINER_OK;
+}
+
+int miner_news_precompute(void* stream, int dtype, const void* news_table, int n_news, const void* packed_weights,
+                          int d, int Dc, int K, float* news_logits, void* news_proj) {
+  if (!news_table || !packed_weights || !news_logits || n_news <= 0) return MINER_EINVAL;
+  const int rc = miner_news_supported(dtype, 1, d, Dc, K);
+  if (rc != MINER_OK) return rc;
+  if (!aligned16(news_table) || !aligned16(packed_weights) || !aligned16(news_logits) || !aligned16(news_proj))
+    return MINER_EALIGN;
+  PreParams prm{news_table, packed_weights, news_logits, news_proj, n_news, d, Dc, K};
+  const int lds = pre_lds(dtype, d, Dc);
+  return dtype == MINER_DTYPE_BF16 ? run_pre<__bf16>(stream, prm, lds) : run_pre<float>(stream, prm, lds);
+}
+
+int miner_score_news(void* stream, int dtype, int score_type, const void* news_table, const float* news_logits,
+                     const void* news_proj, int n_news, const int32_t* his_ids, const uint8_t* his_mask,
+                     const float* his_bias, const int32_t* cand_ids, const int32_t* cand_offsets, int B, int L,
+                     int C, int d, int K, float* scores, float* user_out) {
+  if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
+  if (!news_table || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
+  const int rc = check_news(dtype, L, d, 1, K);
+  if (rc != MINER_OK) return rc;
+  if (score_type == MINER_SCORE_WEIGHTED && !news_proj) return MINER_EINVAL;
+  if (score_type != MINER_SCORE_NONE) {
+    if (!scores || !cand_ids) return MINER_EINVAL;
+    if (!cand_offsets && (C < 0 || C > kMaxCand)) return MINER_ESHAPE;
+  } else if (!user_out) {
+    return MINER_EINVAL;
+  }
+  if (!aligned16(news_table) || !aligned16(news_logits) || !aligned16(news_proj)) return MINER_EALIGN;
+  if (B == 0) return MINER_OK;
+  NsParams prm{news_table, news_logits, news_proj, his_ids, his_mask, his_bias,
+               score_type == MINER_SCORE_NONE ? nullptr : cand_ids,
+               score_type == MINER_SCORE_NONE ? nullptr : cand_offsets,
+               scores, user_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type};
+  return dtype == MINER_DTYPE_BF16 ? launch_score<__bf16>(stream, prm) : launch_score<float>(stream, prm);
+}
+
+}  // extern "C"

@@ -1,0 +1,162 @@
+"""News-side precompute path, backed by libminer_hip.so (include/miner_news.h).
+
+The reference scores an impression from the news encoder's output for its history and candidates
+(src/model/model.py:113-138). Two of its products depend on one news item only:
+
+* ``logits[n] = tanh(W1 e_n) · Qᵀ``   (PolyAttention.forward, model.py:171-174)
+* ``proj[n]   = W2 e_n``              (TargetAwareAttention's linear, model.py:212, before GELU)
+
+Over a news table they are computed once per news item (``precompute``); by linearity
+``mui · W2ᵀ = A · proj[his]``, so ``score`` only gathers rows and runs the contractions over the
+history and the candidates:
+
+    nt = precompute(news_table, packed)          # once per table (or per model update)
+    scores = score(nt, his_ids, his_mask, cand_ids)                  # [B, C] fp32
+    scores, mui = score(nt, ..., return_user=True)                  # + multi_user_interest
+
+Device tensors only: there is no CPU path. float32 is the parity mode, bfloat16 the throughput mode.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from .ops import (PackedWeights, _as_packed, _contig, _dtype_code, _ptr, _require_device, _stream,
+                  check_offsets)
+
+MAX_CAND = 512          # MINER_NEWS_MAX_CAND: candidates per impression
+
+
+@dataclasses.dataclass
+class NewsTable:
+    """A news-embedding table with its per-news precompute (miner_news_precompute output)."""
+    table: Tensor                 # [n_news, d] dtype
+    logits: Tensor                # [n_news, K] fp32
+    proj: Optional[Tensor]        # [n_news, d] dtype, None when built without w_target
+    K: int
+
+    @property
+    def dtype(self) -> torch.dtype:
+        return self.table.dtype
+
+    @property
+    def n_news(self) -> int:
+        return self.table.shape[0]
+
+    @property
+    def d(self) -> int:
+        return self.table.shape[1]
+
+
+def supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int) -> bool:
+    return _lib.lib().miner_news_supported(_dtype_code(dtype), L, d, Dc, K) == 0
+
+
+def _check_shape(dt: int, L: int, d: int, Dc: int, K: int) -> None:
+    code = _lib.lib().miner_news_supported(dt, L, d, Dc, K)
+    if code != 0:
+        raise ValueError(f"news path: L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()} "
+                         "(L <= 64, K <= 32 and K % 4 == 0, d % 64 == 0)")
+
+
+def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = None,
+               w_target: Optional[Tensor] = None, *, with_proj: bool = True,
+               out: Optional[NewsTable] = None) -> NewsTable:
+    """logits = tanh(E·W1ᵀ)·Qᵀ [n_news, K] fp32 and proj = E·W2ᵀ [n_news, d] for a news table
+    (model.py:171-174, :212). ``w_poly`` is a PackedWeights or the raw weights
+    (w_poly [Dc,d], context_codes [K,Dc], w_target [d,d]); ``out`` reuses its buffers."""
+    _require_device(news_table, context_codes, w_target)
+    if not isinstance(w_poly, PackedWeights):
+        _require_device(w_poly)
+    table = _contig(news_table)
+    dtype = table.dtype
+    dt = _dtype_code(dtype)
+    pw = _as_packed(w_poly, context_codes, w_target if with_proj else None, dtype)
+    if with_proj and not pw.has_target:
+        raise ValueError("with_proj needs weights packed with w_target (target_aware_attn.linear.weight)")
+    n_news, d = table.shape
+    if pw.d != d:
+        raise ValueError(f"packed weights are for d={pw.d}, the table has d={d}")
+    _check_shape(dt, 1, d, pw.Dc, pw.K)
+    if out is not None and out.table.data_ptr() == table.data_ptr() and tuple(out.logits.shape) == (n_news, pw.K) \
+            and (out.proj is not None) == with_proj:
+        logits, proj = out.logits, out.proj
+    else:
+        logits = torch.empty((n_news, pw.K), device=table.device, dtype=torch.float32)
+        proj = torch.empty((n_news, d), device=table.device, dtype=dtype) if with_proj else None
+    with torch.cuda.device(table.device):
+        rc = _lib.lib().miner_news_precompute(_stream(table.device), dt, _ptr(table), n_news, _ptr(pw.buf), d,
+                                              pw.Dc, pw.K, _ptr(logits), _ptr(proj))
+    _lib.check(rc, "miner_news_precompute")
+    return NewsTable(table, logits, proj, pw.K)
+
+
+def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[Tensor] = None, *,
+          score_type: str = "weighted", cand_offsets: Optional[Tensor] = None,
+          his_bias: Optional[Tensor] = None, return_user: bool = False, validate: bool = True):
+    """Miner.forward after the news encoder (model.py:113-138) for impressions given as news ids.
+
+    his_ids [B, L] int, his_mask [B, L] bool (True = real click), cand_ids [B, C] (dense) or [N]
+    with cand_offsets [B+1] int32 (ragged), his_bias [B, L] fp32 (category bias averaged over the
+    candidates, model.py:176) or None. Returns scores ([B, C] / [N] fp32) and, if return_user,
+    mui [B, K, d] fp32. score_type 'none' returns mui only. ``validate`` checks ids / offsets.
+    """
+    st = _lib.SCORE_TYPES.get(score_type)
+    if st is None:
+        raise ValueError("Invalid method of aggregating matching score")  # model.py:136
+    _require_device(his_ids, his_mask, cand_ids, cand_offsets, his_bias)
+    dt = _dtype_code(nt.dtype)
+    B, L = his_ids.shape
+    d, K = nt.d, nt.K
+    _check_shape(dt, L, d, 1, K)
+    if st == _lib.SCORE_WEIGHTED and nt.proj is None:
+        raise ValueError("score_type='weighted' needs the table precomputed with w_target (with_proj=True)")
+    dev = nt.table.device
+    hid = _contig(his_ids, torch.int32)
+    mask = _contig(his_mask)
+    if mask.dtype != torch.bool:
+        mask = mask != 0
+    if tuple(mask.shape) != (B, L):
+        raise ValueError(f"his_mask must be [{B},{L}]")
+    mask = mask.view(torch.uint8)
+    if his_bias is not None:
+        his_bias = _contig(his_bias, torch.float32)
+        if tuple(his_bias.shape) != (B, L):
+            raise ValueError(f"his_bias must be [{B},{L}] (category bias averaged over candidates)")
+    cid, offs, C, scores = None, None, 0, None
+    if st != _lib.SCORE_NONE:
+        if cand_ids is None:
+            raise ValueError("cand_ids required")
+        if cand_offsets is None:
+            if cand_ids.dim() != 2 or cand_ids.shape[0] != B:
+                raise ValueError(f"dense cand_ids must be [{B},C]")
+            C = cand_ids.shape[1]
+            if C > MAX_CAND:
+                raise ValueError(f"at most {MAX_CAND} candidates per impression on the news path (got {C})")
+            cid = _contig(cand_ids, torch.int32)
+            scores = torch.empty((B, C), device=dev, dtype=torch.float32)
+        else:
+            cid = _contig(cand_ids.reshape(-1), torch.int32)
+            offs = _contig(cand_offsets, torch.int32)
+            if validate:
+                check_offsets(offs, B, cid.numel())
+                if B and int((offs[1:] - offs[:-1]).max()) > MAX_CAND:
+                    raise ValueError(f"at most {MAX_CAND} candidates per impression on the news path")
+            scores = torch.empty((cid.numel(),), device=dev, dtype=torch.float32)
+    if validate:
+        for ids, what in ((hid, "his_ids"), (cid, "cand_ids")):
+            if ids is not None and ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= nt.n_news):
+                raise ValueError(f"{what} must index the news table [0, {nt.n_news})")
+    mui = torch.empty((B, K, d), device=dev, dtype=torch.float32) if (return_user or st == _lib.SCORE_NONE) else None
+    with torch.cuda.device(dev):
+        rc = _lib.lib().miner_score_news(_stream(dev), dt, st, _ptr(nt.table), _ptr(nt.logits), _ptr(nt.proj),
+                                         nt.n_news, _ptr(hid), _ptr(mask), _ptr(his_bias), _ptr(cid), _ptr(offs),
+                                         B, L, C, d, K, _ptr(scores), _ptr(mui))
+    _lib.check(rc, "miner_score_news")
+    if st == _lib.SCORE_NONE:
+        return mui
+    return (scores, mui) if return_user else scores

@@ -1,0 +1,198 @@
+"""News-side precompute path (miner_news_precompute + miner_score_news) — needs an
+MI355X. The kernel computes the reference's products in a different association
+(mui·W2ᵀ = A·(E·W2ᵀ), logits per news row), so parity is checked against the reference's own
+outputs (golden fixtures, fp32) and the oracle, never bit-for-bit against the dense kernel.
+
+Tolerances (as tests/test_gpu_parity.py):
+* fp32: |x - ref| <= 1e-5*|ref| + 1e-5*rms(ref)   (north_star 1e-5 relative + SURVEY §8c floor)
+* bf16: against the oracle on the same bf16-rounded table and weights, |x - ref| <= 2e-2*|ref| +
+  6e-2*rms(ref) (the kernel rounds the attention weights, proj rows and the GELU output to bf16
+  MFMA operands).
+"""
+import numpy as np
+import pytest
+import torch
+
+from miner_amd import news, ops, synthetic
+from oracle import miner_oracle as orc
+from tests.conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+BF_RTOL, BF_FLOOR = 2e-2, 6e-2
+
+
+def _dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t if dtype is None else t.to(dtype)
+
+
+def _setup(seed, B, L, d, n_news, dtype, C=40, ragged=None, Dc=200, K=32):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    table = (torch.randn((n_news, d), generator=g) / d ** 0.5).to(DEV, dtype)
+    his_ids = torch.randint(0, n_news, (B, L), generator=g)
+    lens = torch.randint(0, L + 1, (B,), generator=g)
+    mask = torch.arange(L)[None, :] >= (L - lens)[:, None]
+    his_ids[~mask] = 0                      # left padding = the pad news (row 0), reader.py:369
+    if ragged:
+        sizes = torch.randint(ragged[0], ragged[1] + 1, (B,), generator=g)
+        offs = torch.zeros(B + 1, dtype=torch.int32)
+        offs[1:] = torch.cumsum(sizes, 0)
+        cand_ids = torch.randint(0, n_news, (int(offs[-1]),), generator=g)
+    else:
+        cand_ids = torch.randint(0, n_news, (B, C), generator=g)
+        offs = None
+    W1, Q, W2 = synthetic.init_weights(seed, d, Dc, K, device=DEV)
+    return (table, his_ids.to(DEV), mask.to(DEV), cand_ids.to(DEV), None if offs is None else offs.to(DEV),
+            W1.to(dtype), Q.to(dtype), W2.to(dtype))
+
+
+def _oracle(table, hid, mask, cid, offs, W1, Q, W2, score_type="weighted", bias=None):
+    """fp32 oracle on the (possibly bf16-rounded) inputs: (mui [B,K,d], scores dense [B,C] / ragged [N])."""
+    T = table.float().cpu()
+    E = T[hid.cpu().long()]
+    m = mask.cpu()
+    w = [x.float().cpu() if x is not None else None for x in (W1, Q, W2)]
+    b = None if bias is None else bias.cpu()
+    if offs is None:
+        return orc.score_torch(E, m, T[cid.cpu().long()], *w, score_type, b)
+    mui = orc.poly_attention_torch(E, m, w[0], w[1], b)
+    o = offs.cpu().tolist()
+    cids = cid.cpu().long()
+    out = []
+    for i in range(len(o) - 1):
+        cd = T[cids[o[i]:o[i + 1]]].unsqueeze(0)
+        if cd.shape[1] == 0:
+            continue
+        _, s = orc.score_torch(E[i:i + 1], m[i:i + 1], cd, *w, score_type, None if b is None else b[i:i + 1])
+        out.append(s.reshape(-1))
+    return mui, torch.cat(out) if out else torch.zeros(0)
+
+
+def _ok(x, ref, dtype, what):
+    x = x.detach().cpu().numpy()
+    ref = ref.detach().cpu().numpy() if isinstance(ref, torch.Tensor) else ref
+    if dtype == torch.float32:
+        ok, worst = orc.parity_ok(x, ref)
+    else:
+        ok, worst = orc.parity_ok(x, ref, rtol=BF_RTOL, rms_floor=BF_FLOOR)
+    assert ok, f"{what}: off by {worst:.2f}x the tolerance"
+    return worst
+
+
+# ---- parity against the reference's own outputs (fp32) ------------------------------------------
+@pytest.mark.parametrize("name", golden_names())
+def test_fp32_matches_reference(name):
+    g = load_golden(name)
+    weighted = g["score_type"] == "weighted"
+    W2 = _dev(g["W2"]) if "W2" in g else None
+    nt = news.precompute(_dev(g["table"]), _dev(g["W1"]), _dev(g["Q"]), W2 if weighted else None, with_proj=weighted)
+    bias = _dev(g["bias"], torch.float32) if g["use_bias"] else None
+    scores, mui = news.score(nt, _dev(g["his_ids"]), _dev(g["his_mask"]), _dev(g["cand_ids"]),
+                             score_type=g["score_type"], his_bias=bias, return_user=True)
+    torch.cuda.synchronize()
+    _ok(scores, g["scores"], torch.float32, f"{name} scores")
+    _ok(mui, g["mui"], torch.float32, f"{name} mui")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("d,Dc,K", [(64, 32, 4), (256, 200, 32), (768, 200, 32), (192, 72, 16)])
+def test_precompute_vs_f64(dtype, d, Dc, K):
+    g = torch.Generator().manual_seed(d + K)
+    n = 333
+    table = (torch.randn((n, d), generator=g) / d ** 0.5).to(DEV, dtype)
+    W1, Q, W2 = [w.to(dtype) for w in synthetic.init_weights(5, d, Dc, K, device=DEV)]
+    nt = news.precompute(table, W1, Q, W2)
+    torch.cuda.synchronize()
+    E = table.double().cpu()
+    logits = torch.tanh(E @ W1.double().cpu().T) @ Q.double().cpu().T
+    proj = E @ W2.double().cpu().T
+    _ok(nt.logits, logits, dtype, "logits")
+    if dtype == torch.float32:
+        _ok(nt.proj.float(), proj, dtype, "proj")
+    else:   # proj is stored in bf16: one rounding of an fp32-accumulated product
+        rel = float((nt.proj.double().cpu() - proj).abs().max() / proj.abs().max())
+        assert rel < 1e-2, rel
+
+
+# ---- shapes and layouts against the oracle --------------------------------------------------------
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,L,d,C,K,Dc", [
+    (300, 50, 768, 40, 32, 200),     # config 3 shape
+    (700, 50, 256, 40, 32, 200),     # config 2 shape, several impressions per workgroup
+    (257, 20, 64, 5, 4, 32),         # config 1 shape: one 64-column chunk (no prefetch overlap)
+    (90, 64, 128, 33, 8, 48),        # L = 64, two chunks
+    (64, 1, 192, 1, 32, 72),         # L = 1, C = 1
+    (40, 37, 320, 150, 12, 64),      # three candidate passes
+])
+def test_vs_oracle(dtype, B, L, d, C, K, Dc):
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(B + d, B, L, d, 2000, dtype, C=C, K=K, Dc=Dc)
+    nt = news.precompute(table, W1, Q, W2)
+    s, mui = news.score(nt, hid, mask, cid, return_user=True)
+    torch.cuda.synchronize()
+    ref_mui, ref = _oracle(table, hid, mask, cid, offs, W1, Q, W2)
+    _ok(s, ref, dtype, "scores")
+    _ok(mui, ref_mui, dtype, "mui")
+
+
+@pytest.mark.parametrize("score_type", ["weighted", "max", "mean"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ragged_bias(score_type, dtype):
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(7, 211, 50, 768, 3000, dtype, ragged=(0, 150))
+    bias = torch.rand(hid.shape, device=DEV) - 0.5
+    w2 = W2 if score_type == "weighted" else None
+    nt = news.precompute(table, W1, Q, w2, with_proj=w2 is not None)
+    s = news.score(nt, hid, mask, cid, score_type=score_type, cand_offsets=offs, his_bias=bias)
+    torch.cuda.synchronize()
+    _, ref = _oracle(table, hid, mask, cid, offs, W1, Q, w2, score_type, bias)
+    _ok(s, ref, dtype, f"{score_type} scores")
+
+
+def test_mui_only_and_all_padded():
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(8, 50, 30, 256, 500, torch.float32)
+    mask[:10] = False                      # all-padded histories: uniform average of pad rows
+    hid[:10] = 0
+    nt = news.precompute(table, W1, Q, W2)
+    mui = news.score(nt, hid, mask, score_type="none")
+    torch.cuda.synchronize()
+    ref_mui, _ = _oracle(table, hid, mask, cid, None, W1, Q, W2)
+    _ok(mui, ref_mui, torch.float32, "mui")
+
+
+def test_launch_invariance_bf16():
+    """A big launch equals the same impressions scored a few at a time (bit-exact: the per-impression
+    arithmetic does not depend on the workgroup an impression lands on)."""
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(9, 3000, 50, 768, 20000, torch.bfloat16)
+    nt = news.precompute(table, W1, Q, W2)
+    big = news.score(nt, hid, mask, cid)
+    parts = torch.cat([news.score(nt, hid[i:i + 37], mask[i:i + 37], cid[i:i + 37]) for i in range(0, 3000, 37)])
+    torch.cuda.synchronize()
+    assert torch.isfinite(big).all()
+    assert torch.equal(big, parts)
+
+
+def test_agrees_with_dense_kernel_bf16():
+    """The news path and the fused dense kernel (weights per impression) on the same inputs agree to
+    bf16 rounding (they round different intermediates)."""
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(10, 200, 50, 768, 4000, torch.bfloat16)
+    nt = news.precompute(table, W1, Q, W2)
+    a = news.score(nt, hid, mask, cid)
+    b = ops.score_gather(table, hid, mask, cid, W1, Q, W2)
+    torch.cuda.synchronize()
+    err = float((a - b).abs().max() / b.pow(2).mean().sqrt())
+    assert err < 0.1, err
+
+
+def test_bad_inputs_raise():
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(11, 8, 10, 256, 100, torch.bfloat16, C=5)
+    nt = news.precompute(table, W1, Q, W2)
+    bad = hid.clone()
+    bad[3, 4] = 100
+    with pytest.raises(ValueError, match="his_ids"):
+        news.score(nt, bad, mask, cid)
+    with pytest.raises(ValueError, match="at most"):
+        news.score(nt, hid, mask, torch.zeros((8, 513), dtype=torch.int32, device=DEV))
+    with pytest.raises(ValueError, match="Invalid method"):
+        news.score(nt, hid, mask, cid, score_type="sum")
+    with pytest.raises(ValueError, match="news path"):
+        news.precompute(table[:, :96].contiguous(), W1[:, :96].contiguous(), Q, None, with_proj=False)
