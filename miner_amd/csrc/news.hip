@@ -32,6 +32,7 @@
 #include <stdint.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/miner_news.h"
 #include "cdna4_common.h"
@@ -88,12 +89,6 @@ __device__ __forceinline__ void dma_b128_c(const void* g, unsigned lds) {
   unsigned t;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(t) : "v"(g), "s"(lds) : "memory");
-}
-#ifndef MINER_NEWS_NT
-#define MINER_NEWS_NT 0
-#endif
-__device__ __forceinline__ void dma_row(const void* g, unsigned lds) {
-  if constexpr (MINER_NEWS_NT) dma_b128(g, lds); else dma_b128_c(g, lds);
 }
 
 // ================================================================================================
@@ -264,6 +259,8 @@ struct NsParams {
   float* scores;
   float* mui_out;
   int n_news, B, L, C, d, K, score_type;
+  int abl;      // ablation bits for diagnosis (MINER_NEWS_ABL): 1 no chunk compute, 2 no row DMAs,
+                // 4 no softmax, 8 no S7, 16 no aux DMAs, 32 no barrier
 };
 
 #ifdef MINER_NEWS_DEBUG
@@ -307,7 +304,9 @@ constexpr int kOffX = kRingB;
 constexpr int kOffLog = kOffX + kXchB;
 constexpr int kOffL1 = kOffLog + 2 * kLogB;
 constexpr int kOffL0 = kOffL1 + 4 * kL1B;
-constexpr int kNewsLds = kOffL0 + 4 * kL0B;
+constexpr int kPrepB = 2 * 64 * 4;                   // softmax coefficients (mul | add) per history slot
+constexpr int kOffPrep = kOffL0 + 4 * kL0B;
+constexpr int kNewsLds = kOffPrep + 2 * kPrepB;
 static_assert(kNewsLds <= kLdsMax, "news_score LDS");
 static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>::NSLOT * NCfg<float>::SLOT == kRingB, "ring");
 
@@ -367,28 +366,72 @@ __device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinter
 __device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B + 768); }
 __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL0 + slot * kL0B); }
 
+// row DMAs of one chunk for this wave (saddr form: the chunk's scalar base + a 32-bit per-lane row
+// offset), parts E[his] / proj[his] / Cand at M0 = mE, mE + PART, mE + 2 PART; one statement, M0
+// saved and restored around it
+#ifndef MINER_NEWS_NT
+#define MINER_NEWS_NT 0
+#endif
+#if MINER_NEWS_NT
+#define NEWS_CP_STR " nt"
+#else
+#define NEWS_CP_STR ""
+#endif
 template <class T>
+__device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC, const char* bE, const char* bY,
+                                          unsigned mE) {
+  using Cf = NCfg<T>;
+  unsigned t;
+  if constexpr (Cf::NI == 1) {
+    asm volatile(
+        "s_nop 4\n\ts_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %4" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(t)
+        : "v"(oH[0]), "v"(oC[0]), "s"(bE), "s"(bY), "s"(mE), "s"(mE + Cf::PART), "s"(mE + 2 * Cf::PART)
+        : "memory");
+  } else {
+    asm volatile(
+        "s_nop 4\n\ts_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %9\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %6" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %10\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %6" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %11\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %12\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %5" NEWS_CP_STR "\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(t)
+        : "v"(oH[0]), "v"(oH[1]), "v"(oC[0]), "v"(oC[1]), "s"(bE), "s"(bY),
+          "s"(mE), "s"(mE + 8192), "s"(mE + Cf::PART), "s"(mE + Cf::PART + 8192),
+          "s"(mE + 2 * Cf::PART), "s"(mE + 2 * Cf::PART + 8192)
+        : "memory");
+  }
+}
+
+template <class T, int ST, bool RAGGED>
 __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cf = NCfg<T>;
+  constexpr int NI = Cf::NI;
+  constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
+  constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
-  const int L = p.L, d = p.d, K = p.K;
+  const int L = p.L, d = p.d;
   const int nchunk = d >> 6;
   const int PD = nchunk < Cf::NSLOT - 1 ? nchunk : Cf::NSLOT - 1;   // chunks in flight
-  const bool weighted = p.score_type == MINER_SCORE_WEIGHTED;
-  const bool ragged = p.cand_off != nullptr;
-  const bool with_cand = p.score_type != MINER_SCORE_NONE;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const T* __restrict__ tab = static_cast<const T*>(p.table);
-  const T* __restrict__ prj = p.proj ? static_cast<const T*>(p.proj) : tab;
+  const char* tabB = static_cast<const char*>(p.table);
+  const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
 
   auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
   // candidates of impression i (scores offset, count <= kMaxCand); L0 must have landed (ragged)
   auto cands = [&](int i, int& off, int& cnt) {
-    if (!with_cand) { off = 0; cnt = 0; return; }
-    if (ragged) {
+    if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
+    if constexpr (RAGGED) {
       const int* o = l0_off(smem, i & 3);
       off = __builtin_amdgcn_readfirstlane(o[0]);
       cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
@@ -398,56 +441,66 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     }
     cnt = min(max(cnt, 0), kMaxCand);
   };
-  auto npass_of = [&](int i) {
-    if (i >= n_i) return 1;
-    int off, cnt;
-    cands(i, off, cnt);
-    return max(1, (cnt + 63) >> 6);
-  };
 
   // ---- aux DMA jobs (issued after a barrier, before that iteration's row DMAs) ----
-  auto issue_L0 = [&](int i) {           // CSR offsets of impression i
-    if (!ragged || i >= n_i || wave != 0) return;
+  auto issue_aux = [&](int i0) {         // L0 (CSR offsets) of i0 + 3, L1 of i0 + 2, L2 of i0 + 1
     const int lane = threadIdx.x & 63;
-    if (lane < 2) dma_b32(p.cand_off + imp_b(i) + lane, sbase + kOffL0 + (i & 3) * kL0B);
-  };
-  auto issue_L1 = [&](int i) {           // ids / mask / bias of impression i (needs L0(i))
-    if (i >= n_i) return;
-    const int lane = threadIdx.x & 63;
-    const int b = imp_b(i);
-    const size_t base = (size_t)b * L + min(lane, L - 1);
-    if (wave == 1) {
-      NEWS_CHK(1, p.his_ids + base, 4, p.his_ids, (size_t)p.B * L * 4, sbase + kOffL1 + (i & 3) * kL1B, 256)
-      dma_b32(p.his_ids + base, sbase + kOffL1 + (i & 3) * kL1B);
-    } else if (wave == 2) {
-      // the aligned word holding mask byte `base` (the reader picks the byte by address)
-      const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
-      NEWS_CHK(2, reinterpret_cast<const void*>(a), 4, p.mask, (size_t)p.B * L + 3, sbase + kOffL1 + (i & 3) * kL1B + 256, 256)
-      dma_b32(reinterpret_cast<const void*>(a), sbase + kOffL1 + (i & 3) * kL1B + 256);
-    } else if (wave == 3) {
-      if (p.bias) dma_b32(p.bias + base, sbase + kOffL1 + (i & 3) * kL1B + 512);
-    } else if (wave >= 4 && with_cand) {   // waves 4..7: candidate ids, 64 per DMA
-      int off, cnt;
-      cands(i, off, cnt);
-      for (int j = wave - 4; 64 * j < cnt; j += 4) {
-        const int c = min(64 * j + lane, cnt - 1);
-        NEWS_CHK(3, p.cand_ids + off + c, 4, p.cand_ids, (size_t)(ragged ? 1 << 30 : p.B * p.C) * 4, sbase + kOffL1 + (i & 3) * kL1B + 768 + 256 * j, 256)
-        dma_b32(p.cand_ids + off + c, sbase + kOffL1 + (i & 3) * kL1B + 768 + 256 * j);
+    if (RAGGED && wave == 0 && i0 + 3 < n_i && lane < 2)
+      dma_b32(p.cand_off + imp_b(i0 + 3) + lane, sbase + kOffL0 + ((i0 + 3) & 3) * kL0B);
+    if (i0 + 2 < n_i) {                  // ids / mask / bias of impression i0 + 2 (needs its L0)
+      const int i = i0 + 2;
+      const size_t base = (size_t)imp_b(i) * L + min(lane, L - 1);
+      const unsigned l1 = sbase + kOffL1 + (i & 3) * kL1B;
+      if (wave == 1) {
+        NEWS_CHK(1, p.his_ids + base, 4, p.his_ids, (size_t)p.B * L * 4, l1, 256)
+        dma_b32(p.his_ids + base, l1);
+      } else if (wave == 2) {
+        // the aligned word holding mask byte `base` (the reader picks the byte by address)
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
+        NEWS_CHK(2, reinterpret_cast<const void*>(a), 4, p.mask, (size_t)p.B * L + 3, l1 + 256, 256)
+        dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
+      } else if (wave == 3) {
+        if (p.bias) dma_b32(p.bias + base, l1 + 512);
+      } else if (WITH_CAND && wave >= 4) {   // waves 4..7: candidate ids, 64 per DMA (j >= 0)
+        int off, cnt;
+        cands(i, off, cnt);
+        for (int j = wave - 4; j >= 0 && 64 * j < cnt; j += 4) {
+          const int c = min(64 * j + lane, cnt - 1);
+          NEWS_CHK(3, p.cand_ids + off + c, 4, p.cand_ids, (size_t)(RAGGED ? 1 << 30 : p.B * p.C) * 4, l1 + 768 + 256 * j, 256)
+          dma_b32(p.cand_ids + off + c, l1 + 768 + 256 * j);
+        }
       }
     }
+    if (i0 + 1 >= 0 && i0 + 1 < n_i) {   // logit rows of impression i0 + 1's history (needs its L1)
+      const int i = i0 + 1;
+      const int row = min(8 * wave + (lane >> 3), L - 1);
+      const int piece = min(lane & 7, (p.K >> 2) - 1);
+      const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
+      NEWS_CHK(4, p.logits + (size_t)id * p.K + 4 * piece, 16, p.logits, (size_t)p.n_news * p.K * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
+      dma_b128_c(p.logits + (size_t)id * p.K + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+    }
   };
-  auto issue_L2 = [&](int i) {           // logit rows of impression i's history (needs L1(i))
-    if (i >= n_i) return;
-    const int lane = threadIdx.x & 63;
-    const int row = min(8 * wave + (lane >> 3), L - 1);
-    const int piece = min(lane & 7, (K >> 2) - 1);
-    const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
-    NEWS_CHK(4, p.logits + (size_t)id * K + 4 * piece, 16, p.logits, (size_t)p.n_news * K * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
-    dma_b128_c(p.logits + (size_t)id * K + 4 * piece,
-               sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+  // masked-softmax coefficients of impression i (needs its L1): s_l = logit_l * mul_l + add_l with
+  // (mul, add) = (1, bias_l) for a click, (0, 1e-30) for a pad slot (model.py:176-180), (0, -inf)
+  // past L; computed by wave 3, read by every wave after the next barrier
+  auto prep_softmax = [&](int i) {
+    if (wave != 3 || i >= n_i) return;
+    const int l = threadIdx.x & 63;
+    const uint32_t mw = l1_mask(smem, i & 3)[l];
+    const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + l) & 3);
+    const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
+    float mul = 0.f, add = -INFINITY;
+    if (l < L) {
+      mul = keep ? 1.f : 0.f;
+      add = keep ? (p.bias ? l1_bias(smem, i & 3)[l] : 0.f) : 1e-30f;
+    }
+    float* pr = reinterpret_cast<float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    pr[l] = mul;
+    pr[64 + l] = add;
   };
-  // rows of chunk `chunk` of pass `pass` of impression i -> ring slot `slot` (3 * NI DMAs per wave)
-  auto issue_rows = [&](int slot, int i, int pass, int chunk) {
+  // this lane's row offsets (bytes, + its swizzled 16-byte piece) for item (i, pass): the history
+  // row (E and proj parts) and the candidate row of each of its NI DMA blocks
+  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC) {
     const int lane = threadIdx.x & 63;
     const bool live = i < n_i;
     int off = 0, cnt = 1;
@@ -455,186 +508,246 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     const int cntp = max(1, min(64, cnt - 64 * pass));
     const int* hid = l1_his(smem, i & 3);
     const int* cid = l1_cand(smem, i & 3);
-    const int piece = lane % Cf::PPR;
+    const uint32_t rowBytes = (uint32_t)d * sizeof(T);
 #pragma unroll
-    for (int part = 0; part < 3; ++part) {
-#pragma unroll
-      for (int jj = 0; jj < Cf::NI; ++jj) {
-        const int blk = wave + 8 * jj;
-        const int rowp = blk * Cf::RPI + lane / Cf::PPR;
-        int id = 0;
-        if (live) id = part < 2 ? hid[min(rowp, L - 1)] : cid[min(64 * pass + min(rowp, cntp - 1), kMaxCand - 1)];
-        id = min(max(id, 0), p.n_news - 1);
-        const T* base = part == 1 ? prj : tab;
-        const char* src = reinterpret_cast<const char*>(base + (size_t)id * d + 64 * chunk) + ((piece ^ nswz<T>(rowp)) << 4);
-        NEWS_CHK(5 + part, src, 16, base, (size_t)p.n_news * d * sizeof(T), sbase + slot * Cf::SLOT + part * Cf::PART + blk * 1024, 1024)
-        dma_row(src, sbase + slot * Cf::SLOT + part * Cf::PART + blk * 1024);
+    for (int jj = 0; jj < NI; ++jj) {
+      const int rowp = (wave + 8 * jj) * Cf::RPI + lane / Cf::PPR;
+      const uint32_t poff = (uint32_t)(((lane % Cf::PPR) ^ nswz<T>(rowp)) << 4);
+      int h = 0, c = 0;
+      if (live) {
+        h = hid[min(rowp, L - 1)];
+        if (WITH_CAND) c = cid[min(64 * pass + min(rowp, cntp - 1), kMaxCand - 1)];
       }
+      h = min(max(h, 0), p.n_news - 1);
+      c = min(max(c, 0), p.n_news - 1);
+      oH[jj] = (uint32_t)h * rowBytes + poff;
+      oC[jj] = (uint32_t)c * rowBytes + poff;
     }
   };
 
-  // ---- prologue: aux for the first impressions, then the first PD chunks ----
-  issue_L0(0); issue_L0(1); issue_L0(2);
-  vm_wait_all();
-  raw_barrier();
-  issue_L1(0); issue_L1(1);
-  vm_wait_all();
-  raw_barrier();
-  issue_L2(0);
-  int qi = 0, qp = 0, qc = 0, qn = npass_of(0);   // issue cursor
-  for (int k = 0; k < PD; ++k) {
-    issue_rows(k, qi, qp, qc);
-    if (++qc == nchunk) { qc = 0; if (++qp == qn) { qp = 0; ++qi; qn = npass_of(qi); } }
+  // ---- per-lane LDS read offsets of this wave's operands (fixed for the whole launch) ----
+  const int P = wave >> 2, sl = (wave >> 1) & 1, ct = wave & 1;
+  uint32_t trOff[8];                   // bf16: transposed part reads, rows 32 ls + .., [ls][s][u]
+  uint32_t cOff[kNQ<T>];               // candidate row 32 ct + pi(r), columns [32 sl + 16 h, +16)
+  {
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 31, h = lane >> 5;
+    if constexpr (sizeof(T) == 2) {
+      const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+      const int col = 32 * sl + 16 * (pp & 1) + 8 * (g & 1) + 4 * (pp >> 1);
+      const int ch = col >> 3, sub = (col & 7) * 2;
+#pragma unroll
+      for (int ls = 0; ls < 2; ++ls)
+#pragma unroll
+        for (int su = 0; su < 4; ++su) {
+          const int row = 32 * ls + 16 * (g >> 1) + 8 * (su >> 1) + 4 * (su & 1) + q;
+          trOff[4 * ls + su] = row * 128 + ((ch ^ nswz<T>(row)) << 4) + sub;
+        }
+    }
+    const int row = 32 * ct + pi_row(r);
+    const int ch0 = sizeof(T) == 2 ? 4 * sl + 2 * h : 8 * sl + 4 * h;
+#pragma unroll
+    for (int q = 0; q < kNQ<T>; ++q) cOff[q] = row * Cf::RB + (((ch0 + q) ^ nswz<T>(row)) << 4);
   }
+
+  // ---- prologue: aux for the first impressions, then the first PD chunks ----
+  if (RAGGED && wave == 0 && (threadIdx.x & 63) < 2)
+    for (int i = 0; i < 3 && i < n_i; ++i)
+      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kOffL0 + i * kL0B);
+  vm_wait_all();
+  raw_barrier();
+  issue_aux(-2);                       // L1 of impression 0 (and L0 of 1, which has landed)
+  vm_wait_all();
+  raw_barrier();
+  issue_aux(-1);                       // L1 of 1, logits of 0
+  prep_softmax(0);
+  vm_wait_all();
+  raw_barrier();
+  uint32_t cH[NI], cC[NI], nH[NI], nC[NI];   // row offsets of the current / next item
+  item_offsets(0, 0, cH, cC);
+  for (int k = 0; k < PD; ++k)
+    if (!(p.abl & 2)) dma_chunk<T>(cH, cC, tabB + k * 64 * sizeof(T), prjB + k * 64 * sizeof(T), sbase + k * Cf::SLOT + wave * 1024);
 
   Frag<T> af[2];                       // attention weights A [K, 64] as two B-operand slabs
   f32x16 acc = zero16();               // this wave's M / Lg partial, one 32x32 candidate tile
-  const int P = wave >> 2, sl = (wave >> 1) & 1, ct = wave & 1;
-  bool pending = false;                // a finished pass waits for S7
-  int pend_off = 0, pend_cnt = 0;
-  int ci = 0, cp = 0, cc = 0, cn = npass_of(0);  // consumer cursor
-  int c_off = 0, c_cnt = 0;
+  int pend_off = -1, pend_cnt = 0;     // a finished pass waiting for S7 (pend_off >= 0)
   int t = 0;
 
   auto s7 = [&]() {
     FRESH_LANE_IDS();
     const int tct = wave & 1, e0 = 4 * (wave >> 1);
     const float* X = reinterpret_cast<const float*>(smem + kOffX);
-    const bool kv = r < K;
+    const bool kv = r < p.K;
 #pragma unroll
     for (int ee = 0; ee < 4; ++ee) {
       const int e = e0 + ee;
       const float m = X[((0 + tct) * 16 + e) * 64 + lane] + X[((2 + tct) * 16 + e) * 64 + lane];
       float sc;
-      if (p.score_type == MINER_SCORE_WEIGHTED) {
+      if constexpr (WEIGHTED) {
         const float lg = X[((4 + tct) * 16 + e) * 64 + lane] + X[((6 + tct) * 16 + e) * 64 + lane];
         const float mx = half_max(kv ? lg : -INFINITY);
         const float pe = kv ? nx_exp<T>(lg - mx) : 0.f;
         const float s = half_sum(pe);
         const float num = half_sum(pe * m);
-        sc = num / s;
-      } else if (p.score_type == MINER_SCORE_MAX) {
-        sc = half_max(kv ? m : -INFINITY);
+        if constexpr (sizeof(T) == 2) sc = num * __builtin_amdgcn_rcpf(s); else sc = num / s;
       } else {
-        sc = half_sum(kv ? m : 0.f) / (float)K;
+        if (p.score_type == MINER_SCORE_MAX) sc = half_max(kv ? m : -INFINITY);
+        else sc = half_sum(kv ? m : 0.f) / (float)p.K;
       }
       const int c = 32 * tct + 16 * h + e;
       if (r == ee && c < pend_cnt) {
-        NEWS_CHK(8, p.scores + pend_off + c, 4, p.scores, (size_t)(ragged ? 1 << 30 : p.B * p.C) * 4, 0, 0)
+        NEWS_CHK(8, p.scores + pend_off + c, 4, p.scores, (size_t)(RAGGED ? 1 << 30 : p.B * p.C) * 4, 0, 0)
         p.scores[pend_off + c] = sc;
       }
     }
   };
 
-  while (ci < n_i) {
-    // slot t landed (this wave's DMAs: all but the PD-1 younger chunks), then for every wave
-    if (PD >= 3) vm_wait<3 * Cf::NI * 2>(); else if (PD == 2) vm_wait<3 * Cf::NI>(); else vm_wait<0>();
-    raw_barrier();
-    const bool first = cp == 0 && cc == 0;
-    if (first) {
-      issue_L0(ci + 3);
-      issue_L1(ci + 2);
-      issue_L2(ci + 1);
+  // one 64-column chunk of item (ci, cp): wait for its slot, the row DMAs PD chunks ahead, the X /
+  // mui slab and the candidate product. `mode`: 1 X, 2 candidate product, 4 mui out
+  auto chunk = [&](int ci, int cc, int mode, int ni, int np) {
+    // row DMAs PD chunks ahead (into the next item near the end of this one)
+    {
+      const int ic = cc + PD;
+      if (ic == nchunk) item_offsets(ni, np, nH, nC);
+      const bool nx = ic >= nchunk;
+      const int ch = nx ? ic - nchunk : ic;
+      if (!(p.abl & 2))
+        dma_chunk<T>(nx ? nH : cH, nx ? nC : cC, tabB + ch * 64 * sizeof(T), prjB + ch * 64 * sizeof(T),
+                     sbase + ((t + PD) % Cf::NSLOT) * Cf::SLOT + wave * 1024);
     }
-    const bool did_s7 = pending && with_cand;
-    if (did_s7) s7();
-    pending = false;
-    issue_rows((t + PD) % Cf::NSLOT, qi, qp, qc);
-    if (++qc == nchunk) { qc = 0; if (++qp == qn) { qp = 0; ++qi; qn = npass_of(qi); } }
-
-    if (first) {
-      // ---- attention weights of impression ci: softmax over the history (model.py:176-181) ----
-      FRESH_LANE_IDS();
-      const int b = imp_b(ci);
-      const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (ci & 1) * kLogB);
-      const uint32_t* mw = l1_mask(smem, ci & 3);
-      const float* bs = l1_bias(smem, ci & 3);
-      float v[32];
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const int l = 32 * (j >> 4) + 16 * h + (j & 15);
-        float s = -INFINITY;
-        if (l < L) {
-          s = lgb[l * 32 + r];
-          if (p.bias) s += bs[l];
-          const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)b * L + l) & 3);
-          if (((mw[l] >> (8 * a)) & 0xffu) == 0u) s = 1e-30f;      // masked_fill_(~mask, 1e-30)
-        }
-        v[j] = s;
-        mx = fmaxf(mx, s);
-      }
-      mx = both_max(mx);
-      float sum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const int l = 32 * (j >> 4) + 16 * h + (j & 15);
-        v[j] = l < L ? nx_exp<T>(v[j] - mx) : 0.f;
-        sum += v[j];
-      }
-      sum = both_sum(sum);
-      const float inv = r < K ? 1.0f / sum : 0.f;
-#pragma unroll
-      for (int ls = 0; ls < 2; ++ls) {
-        if constexpr (sizeof(T) == 2) {
-#pragma unroll
-          for (int m = 0; m < 8; ++m) af[ls].q[m >> 2][m & 3] = pack_bf16x2(v[16 * ls + 2 * m] * inv, v[16 * ls + 2 * m + 1] * inv);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) af[ls].q[e >> 2][e & 3] = __float_as_uint(v[16 * ls + e] * inv);
-        }
-      }
-    }
-    if (cc == 0) {
-      acc = zero16();
-      cands(ci, c_off, c_cnt);
-    }
-    const int cntp = min(64, c_cnt - 64 * cp);
-
-    // ---- this chunk: X / mui slab, then the candidate product ----
-    const bool need_x = (P == 0) ? (with_cand || (p.mui_out && cp == 0)) : weighted;
-    const bool need_c = with_cand && (ct == 0 || cntp > 32) && (P == 0 || weighted);
-    const bool need_mui = P == 0 && p.mui_out && cp == 0 && ct == 0;
-    if (need_x && (need_c || need_mui)) {
+    if (mode & 1) {
       FRESH_LANE_IDS();
       const char* slot = smem + (t % Cf::NSLOT) * Cf::SLOT;
+      const char* part = slot + P * Cf::PART;
       f32x16 ax = zero16();
 #pragma unroll
       for (int ls = 0; ls < 2; ++ls) {
         Frag<T> ef;
-        load_partT<T>(ef, slot + P * Cf::PART, ls, sl, lane);
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int su = 0; su < 4; ++su) {
+            const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds_char*)(part + trOff[4 * ls + su]));
+            const auto w2 = __builtin_bit_cast(uint2, v);
+            ef.q[su >> 1][2 * (su & 1)] = w2.x;
+            ef.q[su >> 1][2 * (su & 1) + 1] = w2.y;
+          }
+        } else {
+          load_partT<T>(ef, part, ls, sl, lane);
+        }
         mma_slab(ax, ef, af[ls]);
       }
-      if (need_mui && r < K) {
-        float* dst = p.mui_out + ((size_t)imp_b(ci) * K + r) * d + 64 * cc + 32 * sl + 16 * h;
+      if ((mode & 4) && r < p.K) {
+        float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + r) * d + 64 * cc + 32 * sl + 16 * h;
 #pragma unroll
         for (int e = 0; e < 16; e += 4) *reinterpret_cast<float4*>(dst + e) = make_float4(ax[e], ax[e + 1], ax[e + 2], ax[e + 3]);
       }
-      if (need_c) {
-        if (P == 1) gelu_tile<T>(ax);
+      if (mode & 2) {
+        if (WEIGHTED && P == 1) gelu_tile<T>(ax);
         Frag<T> xf, cf;
         acc_to_frag<T>(xf, ax);
-        load_cand<T>(cf, slot + 2 * Cf::PART, ct, sl, lane);
+        const char* cpart = slot + 2 * Cf::PART;
+#pragma unroll
+        for (int q = 0; q < kNQ<T>; ++q) cf.q[q] = lds_u32x4(cpart + cOff[q]);
         mma_slab(acc, cf, xf);
       }
     }
+  };
+  auto wait_slot = [&]() {
+    // slot t landed (this wave's DMAs: all but the PD-1 younger chunks), then for every wave
+    if (PD >= 3) vm_wait<3 * NI * 2>(); else if (PD == 2) vm_wait<3 * NI>(); else vm_wait<0>();
+    raw_barrier();
+  };
 
-    if (cc == nchunk - 1) {            // pass done: partials -> LDS, S7 next iteration
-      if (nchunk == 1 && did_s7) raw_barrier();
-      const int lane = threadIdx.x & 63;
-      float* dst = reinterpret_cast<float*>(smem + kOffX) + (wave * 16) * 64 + lane;
+  for (int ci = 0; ci < n_i; ++ci) {
+    int c_off, c_cnt;
+    cands(ci, c_off, c_cnt);
+    const int cn = max(1, (c_cnt + 63) >> 6);
+    for (int cp = 0; cp < cn; ++cp) {
+      const int cntp = min(64, c_cnt - 64 * cp);
+      const bool need_c = WITH_CAND && (ct == 0 || cntp > 32) && (P == 0 || WEIGHTED);
+      const bool need_mui = P == 0 && p.mui_out != nullptr && cp == 0 && ct == 0;
+      const bool need_x = (P == 0) ? (WITH_CAND || need_mui) : WEIGHTED;
+      const int mode = (p.abl & 1) ? 0 : ((need_x && (need_c || need_mui)) ? 1 : 0) | (need_c ? 2 : 0) | (need_mui ? 4 : 0);
+      // the item after this one, for the DMAs that run ahead into it
+      const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
+
+      // ---- first chunk of the item, with the per-item work ----
+      wait_slot();
+      if (cp == 0) issue_aux(ci);
+      const bool did_s7 = WITH_CAND && pend_off >= 0;
+      if (did_s7) s7();
+      pend_off = -1;
+      if (cp == 0) {
+        prep_softmax(ci + 1);
+        // ---- attention weights of impression ci: softmax over the history (model.py:176-181) ----
+        FRESH_LANE_IDS();
+        const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (ci & 1) * kLogB);
+        const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (ci & 1) * kPrepB);
+        float v[32];
+        float mx = -INFINITY;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) dst[e * 64] = acc[e];
-      pending = true;
+        for (int ls = 0; ls < 2; ++ls) {
+#pragma unroll
+          for (int j4 = 0; j4 < 4; ++j4) {
+            const int l0 = 32 * ls + 16 * h + 4 * j4;
+            const float4 mu = *reinterpret_cast<const float4*>(pr + l0);
+            const float4 ad = *reinterpret_cast<const float4*>(pr + 64 + l0);
+            const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float s = __builtin_fmaf(lgb[(l0 + u) * 32 + r], m4[u], a4[u]);
+              v[16 * ls + 4 * j4 + u] = s;
+              mx = fmaxf(mx, s);
+            }
+          }
+        }
+        mx = both_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          v[j] = nx_exp<T>(v[j] - mx);     // exp(-inf) = 0 past L
+          sum += v[j];
+        }
+        sum = both_sum(sum);
+        float inv;
+        if constexpr (sizeof(T) == 2) inv = __builtin_amdgcn_rcpf(sum); else inv = 1.0f / sum;
+        if (r >= p.K) inv = 0.f;
+#pragma unroll
+        for (int ls = 0; ls < 2; ++ls) {
+          if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) af[ls].q[m >> 2][m & 3] = pack_bf16x2(v[16 * ls + 2 * m] * inv, v[16 * ls + 2 * m + 1] * inv);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) af[ls].q[e >> 2][e & 3] = __float_as_uint(v[16 * ls + e] * inv);
+          }
+        }
+      }
+      acc = zero16();
+      chunk(ci, 0, mode, ni, np);
+      ++t;
+      // ---- the other chunks ----
+      for (int cc = 1; cc < nchunk; ++cc, ++t) {
+        wait_slot();
+        chunk(ci, cc, mode, ni, np);
+      }
+      // pass done: partials -> LDS, S7 at the next item's first chunk
+      if (nchunk == 1 && did_s7) raw_barrier();
+      {
+        const int lane = threadIdx.x & 63;
+        float* dst = reinterpret_cast<float*>(smem + kOffX) + (wave * 16) * 64 + lane;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) dst[e * 64] = acc[e];
+      }
       pend_off = c_off + 64 * cp;
       pend_cnt = cntp;
+#pragma unroll
+      for (int jj = 0; jj < NI; ++jj) { cH[jj] = nH[jj]; cC[jj] = nC[jj]; }
     }
-    ++t;
-    if (++cc == nchunk) { cc = 0; if (++cp == cn) { cp = 0; ++ci; cn = npass_of(ci); } }
   }
   vm_wait_all();
   raw_barrier();
-  if (pending && with_cand) s7();
+  if (WITH_CAND && pend_off >= 0) s7();
 }
 
 // ================================================================================================
@@ -693,7 +806,13 @@ int run_pre(void* stream, const PreParams& prm, int lds) {
 
 template <class T>
 int launch_score(void* stream, const NsParams& prm) {
-  auto kern = news_score<T>;
+  void (*kern)(NsParams) = nullptr;
+  const bool rg = prm.cand_off != nullptr;
+  switch (prm.score_type) {
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true> : news_score<T, MINER_SCORE_WEIGHTED, false>; break;
+    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false>; break;
+    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true> : news_score<T, MINER_SCORE_MAX, false>; break;
+  }
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kNewsLds);
   if (e != hipSuccess) return (int)e;
   int grid = num_cus();
@@ -751,10 +870,12 @@ int miner_score_news(void* stream, int dtype, int score_type, const void* news_t
   }
   if (!aligned16(news_table) || !aligned16(news_logits) || !aligned16(news_proj)) return MINER_EALIGN;
   if (B == 0) return MINER_OK;
+  const char* abl = getenv("MINER_NEWS_ABL");
   NsParams prm{news_table, news_logits, news_proj, his_ids, his_mask, his_bias,
                score_type == MINER_SCORE_NONE ? nullptr : cand_ids,
                score_type == MINER_SCORE_NONE ? nullptr : cand_offsets,
-               scores, user_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type};
+               scores, user_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type,
+               abl ? atoi(abl) : 0};
   return dtype == MINER_DTYPE_BF16 ? launch_score<__bf16>(stream, prm) : launch_score<float>(stream, prm);
 }
 
