@@ -1,19 +1,23 @@
-"""Benchmark: scored (user, candidate) pairs/s of the fused MINER scoring kernel on MI355X.
+"""Benchmark: scored (user, candidate) pairs/s of the MINER scoring path on MI355X.
 
     python bench.py [--gpus N --steps K --warmup W]            # N=1 default
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Workload (BASELINE.json metric, config 3 "MIND-large shape"): history L=50, K=32 interests,
-d=768, Dc=200, C=40 candidates per impression, bf16 operands / fp32 accumulation, synthetic
-impressions already resident in HBM. One step = one launch of the fused kernel over a batch of
-``--batch`` impressions per GPU; impressions are sharded across ranks with no collective on the
-data path (weak scaling); ``value`` = pairs scored by all ranks / max-over-ranks time.
+d=768, Dc=200, C=40 candidates per impression, bf16 operands / fp32 accumulation. Impressions
+are given as news ids over a 104,000 x 768 news table (the reference's eval input: reader.py
+feeds news ids, the news encoder's output is a per-news table), ids and table resident in HBM.
+One step = the per-news precompute over the WHOLE table (news_pre: tanh(E·W1ᵀ)·Qᵀ and E·W2ᵀ,
+SURVEY.md §8 f2) + one launch of the scoring kernel (news_score) over ``--batch`` impressions per
+GPU; impressions are sharded across ranks with no collective on the data path (weak scaling);
+``value`` = pairs scored by all ranks / max-over-ranks time.
 
-Also reported (same JSON line): the roofline of the dominant kernel (algorithmic FLOPs / bytes per
-launch over the HIP-event launch time, on the stream the kernel is launched on), the fp32 parity
-mode's throughput, and the CPU baseline (the oracle — a restatement of the reference's torch CPU
-path — timed on this host's cores over a bounded sample) on rank 0 at N=1.
+Also reported (same JSON line): the HBM roofline of the scoring kernel (algorithmic bytes per
+launch over its HIP-event launch time, on the stream it runs on), the precompute's time, the fp32
+parity mode, the fused dense-row kernel (``--workload config3-dense``: weights per impression, rows
+given as [B, L, d] tensors) for comparison, and the CPU baseline (the oracle — a restatement of
+the reference's torch CPU path — timed on this host's cores over a bounded sample) at N=1.
 
 ``--workload fastformer`` measures BASELINE config 4 instead (the FastFormer user encoder,
 SURVEY.md §8 f3): 50,000 impressions per GPU per step, history 50, 40 candidates, hidden 256,
@@ -232,6 +236,185 @@ def run_fastformer(args, rank, world, dev):
         dist.destroy_process_group()
 
 
+N_NEWS = 104_000     # MIND-large-shaped news table (~104k news x 768)
+NEWS_B = 131_072     # impressions per GPU per step (news-id input: 47 MB of ids per batch)
+
+
+def news_bytes_per_impression(L, d, C, K, elem):
+    """Algorithmic bytes of the news-path scoring kernel per impression: the gathered history rows
+    of the table and of its projection, the candidate rows, the history logit rows (fp32), the ids,
+    the mask and the fp32 scores (the per-news precompute is a separate launch)."""
+    return 2 * L * d * elem + C * d * elem + L * K * 4 + 4 * L + L + 4 * C + 4 * C
+
+
+def news_precompute_flops(n_news, d, Dc, K):
+    """tanh(E·W1ᵀ)·Qᵀ and E·W2ᵀ over the table (model.py:171-174, :212)."""
+    return n_news * (2 * d * Dc + 2 * Dc * K + 2 * d * d)
+
+
+def load_news_traffic(path, B):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_bf16" and t.get("batch") == B:
+            return t
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def news_batch(seed, B, dev):
+    """Impressions as news ids (the reference's eval input, reader.py:351-379): history length
+    ~ U{0..L}, left-padded with the pad news (row 0, reader.py:101-110, :369); candidates uniform."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    lens = torch.randint(0, L + 1, (B,), generator=g, device=dev)
+    mask = torch.arange(L, device=dev)[None, :] >= (L - lens)[:, None]
+    hid = torch.randint(1, N_NEWS, (B, L), generator=g, device=dev, dtype=torch.int32)
+    hid[~mask] = 0
+    cid = torch.randint(1, N_NEWS, (B, C), generator=g, device=dev, dtype=torch.int32)
+    return hid, mask, cid
+
+
+def dense_kernel_line(dev, B=32768, steps=5):
+    """The fused dense-row kernel (weights per impression, miner_score) on the same shape, for
+    comparison: pairs/s and its MFMA fraction."""
+    from miner_amd import ops, synthetic
+    imp = synthetic.impressions(36, 0, B, L=L, d=D, C=C, device=dev, dtype=torch.bfloat16)
+    W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
+    pw = ops.pack_weights(W1, Q, W2, dtype=torch.bfloat16)
+    ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / steps
+    tf = flops_per_impression(L, K, D, DC, C) * B / (ms / 1e3) / 1e12
+    del imp
+    return {"kernel": "miner_fused<bf16,full>", "value": round(B * C / (ms / 1e3), 1), "unit": "pairs/s",
+            "ms_per_launch": round(ms, 4), "impressions": B, "tflops": round(tf, 2),
+            "frac_bf16_peak": round(tf / PEAK_BF16_TFLOPS, 4)}
+
+
+def run_news(args, rank, world, dev):
+    """BASELINE config 3 on the news-id input: every step recomputes the per-news
+    precompute over the whole table (news_pre) and scores a batch of impressions (news_score)."""
+    from miner_amd import news, ops, synthetic
+    B = args.batch if args.batch_set else NEWS_B
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(36)
+    table = (torch.randn((N_NEWS, D), generator=g, device=dev) / D ** 0.5).to(bf)
+    W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
+    pw16 = ops.pack_weights(W1, Q, W2, dtype=bf)        # once per model, outside the timed region
+    pool = [news_batch(36 + (rank * args.pool + p) * B, B, dev) for p in range(args.pool)]
+    nt = news.precompute(table, pw16)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i, ev=None):
+        nonlocal nt
+        hid, mask, cid = pool[i % len(pool)]
+        if ev is not None:
+            ev[0].record(stream)
+        nt = news.precompute(table, pw16, out=nt)
+        if ev is not None:
+            ev[1].record(stream)
+        out = news.score(nt, hid, mask, cid, validate=False)
+        if ev is not None:
+            ev[2].record(stream)
+        return out
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = step(i, ev[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    pre_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    kern_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out).all()
+
+    # fp32 parity mode of the same path (fewer steps; 32k impressions)
+    f32 = None
+    if args.fp32_steps > 0:
+        n32 = min(B, 32768)
+        hid, mask, cid = [x[:n32] for x in pool[0]]
+        t32 = table.float()
+        pw32 = ops.pack_weights(W1, Q, W2, dtype=torch.float32)
+        nt32 = news.precompute(t32, pw32)
+        news.score(nt32, hid, mask, cid, validate=False)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(args.fp32_steps):
+            nt32 = news.precompute(t32, pw32, out=nt32)
+            news.score(nt32, hid, mask, cid, validate=False)
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms32 = a.elapsed_time(b) / args.fp32_steps
+        f32 = {"value": round(n32 * C / (ms32 / 1e3), 1), "unit": "pairs/s", "ms_per_step": round(ms32, 3),
+               "impressions": n32, "note": "news path, fp32 operands and arithmetic (the parity mode)"}
+        del t32, nt32
+    dense = None
+    if world == 1 and not args.no_dense:
+        dense = dense_kernel_line(dev)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    value = B * C * args.steps * world / elapsed
+    by = news_bytes_per_impression(L, D, C, K, 2) * B
+    gbs = by / (kern_ms / 1e3) / 1e9
+    traffic = load_news_traffic(args.news_traffic, B)
+    roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+            "kernel": "news_score<bf16,weighted>", "algorithmic_bytes_per_launch": by,
+            "kernel_ms": round(kern_ms, 4),
+            "note": "algorithmic bytes = gathered rows (history of the table and of its projection, "
+                    "candidates) + logit rows + ids + mask + scores; traffic = PMC HBM bytes per launch "
+                    "(rows re-read by other impressions hit L2 / the Infinity Cache)"}
+    pre_fl = news_precompute_flops(N_NEWS, D, DC, K)
+    pre = {"kernel": "news_pre<bf16>", "ms": round(pre_ms, 4), "flops": pre_fl,
+           "tflops": round(pre_fl / (pre_ms / 1e3) / 1e12, 2),
+           "frac_bf16_peak": round(pre_fl / (pre_ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+    cpu = cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
+    line = {
+        "metric": "(user,candidate) scores/sec at history=50,K=32,d=768; AUC parity vs ref",
+        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (seeded MIND-large-shaped impressions as news ids over a random news table; "
+                "random-init weights)",
+        "config": {"workload": "config 3 MIND-large shape, news-id input (per step: per-news precompute "
+                               "over the whole table + scoring)",
+                   "history": L, "K": K, "d": D, "Dc": DC, "candidates": C, "news_table": N_NEWS,
+                   "impressions_per_gpu_per_step": B, "global_batch": B * world,
+                   "parallelism": f"dp{world} (impression shards, no data-path collective)"},
+        "roofline": roof, "precompute": pre, "fp32_parity_mode": f32, "dense_rows_kernel": dense,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def load_traffic(path):
     try:
         with open(path) as f:
@@ -248,13 +431,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="config3", choices=["config3", "fastformer"])
+    ap.add_argument("--workload", default="config3", choices=["config3", "config3-dense", "fastformer"])
     ap.add_argument("--batch", type=int, default=None, help="impressions per GPU per step")
     ap.add_argument("--pool", type=int, default=2, help="distinct resident batches per GPU")
     ap.add_argument("--fp32-steps", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--news-traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_news.json"))
+    ap.add_argument("--no-dense", action="store_true", help="skip the dense-row kernel comparison")
     args = ap.parse_args()
     args.batch_set = args.batch is not None
     if args.batch is None:
@@ -269,6 +454,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     if args.workload == "fastformer":
         return run_fastformer(args, rank, world, dev)
+    if args.workload == "config3":
+        return run_news(args, rank, world, dev)
 
     from miner_amd import ops, synthetic
 

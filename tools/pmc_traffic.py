@@ -23,6 +23,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL_TAG = "miner_fusedIDF16bLi0E"     # mangled miner_fused<__bf16, kFull, ...>
+KERNEL_TAGS = [KERNEL_TAG, "miner_fused<__bf16, 0"]
 
 
 def read_counters(d):
@@ -32,7 +33,7 @@ def read_counters(d):
         with open(path) as f:
             for row in csv.DictReader(f):
                 kn = row.get("Kernel_Name", "")
-                if KERNEL_TAG not in kn and "miner_fused<__bf16, 0" not in kn:
+                if not any(tag in kn for tag in KERNEL_TAGS):
                     continue
                 did = row.get("Dispatch_Id") or row.get("Correlation_Id")
                 per[did][row["Counter_Name"]] += float(row["Counter_Value"])
@@ -51,7 +52,15 @@ def main():
     ap.add_argument("--cus", type=int, default=256)
     ap.add_argument("--xcds", type=int, default=8)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--news", action="store_true",
+                    help="the news-path scoring kernel news_score<bf16, weighted, dense> (bench.py config3)")
     args = ap.parse_args()
+    workload, kernel = "L50_K32_d768_Dc200_C40_bf16", "miner_fused<bf16,full>"
+    if args.news:
+        KERNEL_TAGS[:] = ["news_scoreIDF16bLi0ELb0E", "news_score<__bf16, 0, false>"]
+        workload, kernel = "news_L50_K32_d768_C40_N104000_bf16", "news_score<bf16,weighted>"
+        if args.out == os.path.join(ROOT, "profiles", "pmc_traffic.json"):
+            args.out = os.path.join(ROOT, "profiles", "pmc_traffic_news.json")
     med, n = {}, {}
     for d in args.dirs:
         if not os.path.isdir(d):
@@ -60,11 +69,11 @@ def main():
         med.update(m)
         n[d] = k
     if "FETCH_SIZE" not in med or "WRITE_SIZE" not in med:
-        sys.exit(f"missing FETCH_SIZE/WRITE_SIZE for {KERNEL_TAG}: found {sorted(med)} ({n})")
+        sys.exit(f"missing FETCH_SIZE/WRITE_SIZE for {KERNEL_TAGS}: found {sorted(med)} ({n})")
     fetch = 2 * med["FETCH_SIZE"] * 1024
     write = med["WRITE_SIZE"] * 1024
     res = {
-        "workload": "L50_K32_d768_Dc200_C40_bf16", "batch": args.batch, "kernel": "miner_fused<bf16,full>",
+        "workload": workload, "batch": args.batch, "kernel": kernel,
         "dispatches": n, "FETCH_SIZE_KiB": med["FETCH_SIZE"], "WRITE_SIZE_KiB": med["WRITE_SIZE"],
         "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,
