@@ -19,7 +19,9 @@ parity mode, the fused dense-row kernel (``--workload config3-dense``: weights p
 given as [B, L, d] tensors) for comparison, and the CPU baseline (the oracle — a restatement of
 the reference's torch CPU path — timed on this host's cores over a bounded sample) at N=1.
 
-``--workload fastformer`` measures BASELINE config 4 instead (the FastFormer user encoder,
+``--workload corpus`` measures BASELINE config 5 (every user against a 200k-news table, history 200,
+K=64, fp16, fused click score + top-k); ``--workload fastformer`` measures
+BASELINE config 4 instead (the FastFormer user encoder,
 SURVEY.md §8 f3): 50,000 impressions per GPU per step, history 50, 40 candidates, hidden 256,
 bf16, same JSON contract.
 """
@@ -415,6 +417,124 @@ def run_news(args, rank, world, dev):
         dist.destroy_process_group()
 
 
+C5_L, C5_K, C5_N, C5_U, C5_TOPK = 200, 64, 200_000, 2048, 100
+
+
+def corpus_cpu_baseline(seconds: float = 10.0):
+    """Config-5 oracle (the reference's encoder + click score restated in torch fp32 on the CPU,
+    oracle/corpus_oracle.py) on host cores: 8 users against news chunks of 4096 until `seconds`."""
+    from miner_amd import synthetic
+    from oracle import corpus_oracle as co
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(5)
+    U = 8
+    news = torch.randn((16384, D), generator=g) / D ** 0.5
+    E = news[torch.randint(0, 16384, (U, C5_L), generator=g)]
+    mask = torch.rand((U, C5_L), generator=g) > 0.2
+    W1, Q, W2 = synthetic.init_weights(5, D, DC, C5_K)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        mui, proj = co.encode(E, mask, W1, Q, W2)
+        pairs, i = 0, 0
+        while True:
+            lo = (i * 4096) % 16384
+            co.corpus_scores(mui, proj, news[lo:lo + 4096])
+            pairs += U * 4096
+            i += 1
+            el = time.perf_counter() - t0
+            if el > seconds and i >= 2:
+                break
+    return {"value": round(pairs / el, 1), "unit": "(user,news) pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{U} users (history {C5_L}, K={C5_K}, d={D}) encoded and scored against {pairs // U} news "
+                      f"rows in chunks of 4096, fp32, {el:.1f}s (top-k selection not included)"}
+
+
+def run_corpus(args, rank, world, dev):
+    """BASELINE config 5: every user against the whole 200k-news table (fp16), history 200, K=64,
+    fused click score + running top-k (never materialising the U x N scores). One step = encode
+    ``--batch`` users (default 2048) per GPU and rank them against the table; users shard over
+    ranks (weak scaling, no data-path collective)."""
+    from miner_amd import corpus, synthetic
+    U = args.batch if args.batch_set else C5_U
+    dt = torch.float16
+    g = torch.Generator(device=dev).manual_seed(5)
+    table = (torch.randn((C5_N, D), generator=g, device=dev) / D ** 0.5).to(dt)
+    W1, Q, W2 = synthetic.init_weights(5, D, DC, C5_K, device=dev)
+    pk = corpus.pack_encoder(W1, Q, W2, dtype=dt)
+    pool = []
+    for p in range(args.pool):
+        gg = torch.Generator(device=dev).manual_seed(1000 + rank * args.pool + p)
+        hid = torch.randint(0, C5_N, (U, C5_L), generator=gg, device=dev, dtype=torch.int32)
+        lens = torch.randint(1, C5_L + 1, (U,), generator=gg, device=dev)
+        mask = torch.arange(C5_L, device=dev)[None, :] >= (C5_L - lens)[:, None]
+        pool.append((hid, mask))
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i, ev=None):
+        hid, mask = pool[i % len(pool)]
+        if ev is not None:
+            ev[0].record(stream)
+        mui, proj = corpus.encode_users(table, mask, pk, his_ids=hid)
+        if ev is not None:
+            ev[1].record(stream)
+        out = corpus.rank_topk(mui, proj, table, C5_TOPK)
+        if ev is not None:
+            ev[2].record(stream)
+        return out
+
+    steps = args.steps if args.steps_set else 5
+    warm = args.warmup if args.warmup_set else 1
+    for i in range(warm):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        out = step(i, ev[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+    rank_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out[0]).all()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    pairs = U * C5_N
+    fl = pairs * 4 * C5_K * D            # M = mui·e and Lg = proj·e per (user, news) pair (model.py:127, :213)
+    tflops = fl / (rank_ms / 1e3) / 1e12
+    enc_fl = U * (2 * C5_L * D * DC + 2 * C5_L * DC * C5_K + 2 * C5_K * C5_L * D + 2 * C5_K * D * D)
+    line = {
+        "metric": "(user,news) click scores/sec, full-corpus ranking with fused top-k (config 5)",
+        "value": round(pairs * steps * world / elapsed, 1), "unit": "pairs/s", "n_gpus": world, "steps": steps,
+        "warmup": warm, "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+        "data": "synthetic (random news table and user histories, random-init weights)",
+        "config": {"workload": "config 5 full-corpus ranking stress", "news": C5_N, "history": C5_L, "K": C5_K,
+                   "d": D, "Dc": DC, "topk": C5_TOPK, "users_per_gpu_per_step": U, "global_users_per_step": U * world,
+                   "parallelism": f"dp{world} (user shards, news table replicated, no data-path collective)"},
+        "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": "rk_fused<fp16>",
+                     "flops_per_launch": fl, "kernel_ms": round(rank_ms, 3)},
+        "encoder": {"kernel": "ue_fused<fp16>", "ms": round(enc_ms, 3),
+                    "tflops": round(enc_fl / (enc_ms / 1e3) / 1e12, 2)},
+        "cpu_baseline": corpus_cpu_baseline(min(args.cpu_seconds, 10.0)) if (world == 1 and not args.no_cpu) else None,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def load_traffic(path):
     try:
         with open(path) as f:
@@ -431,7 +551,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="config3", choices=["config3", "config3-dense", "fastformer"])
+    ap.add_argument("--workload", default="config3", choices=["config3", "config3-dense", "fastformer", "corpus"])
     ap.add_argument("--batch", type=int, default=None, help="impressions per GPU per step")
     ap.add_argument("--pool", type=int, default=2, help="distinct resident batches per GPU")
     ap.add_argument("--fp32-steps", type=int, default=2)
@@ -442,6 +562,8 @@ def main():
     ap.add_argument("--no-dense", action="store_true", help="skip the dense-row kernel comparison")
     args = ap.parse_args()
     args.batch_set = args.batch is not None
+    args.steps_set = "--steps" in sys.argv
+    args.warmup_set = "--warmup" in sys.argv
     if args.batch is None:
         args.batch = 32768
 
@@ -456,6 +578,8 @@ def main():
         return run_fastformer(args, rank, world, dev)
     if args.workload == "config3":
         return run_news(args, rank, world, dev)
+    if args.workload == "corpus":
+        return run_corpus(args, rank, world, dev)
 
     from miner_amd import ops, synthetic
 
