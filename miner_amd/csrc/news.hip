@@ -80,6 +80,16 @@ __device__ __forceinline__ float both_sum(float x) {
   return __uint_as_float(s[0]) + __uint_as_float(s[1]);
 }
 
+// all-reduce over the 4 16-lane rows (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float rows4_max(float x) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return both_max(fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1])));
+}
+__device__ __forceinline__ float rows4_sum(float x) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return both_sum(__uint_as_float(s[0]) + __uint_as_float(s[1]));
+}
+
 __device__ __forceinline__ uint32_t lds_u32(const char* p) { return *reinterpret_cast<const uint32_t*>(p); }
 __device__ __forceinline__ u32x4 lds_u32x4(const char* p) { return *reinterpret_cast<const u32x4*>(p); }
 
@@ -296,17 +306,18 @@ template <class T> struct NCfg {
 
 // LDS carve (bytes): [ring | xchg | logit blocks x2 | aux L1 x4 | aux L0 x4]
 constexpr int kRingB = 98304;                        // NSLOT * SLOT for both dtypes
-constexpr int kXchB = kWaves * 16 * 64 * 4;
-constexpr int kLogB = 64 * 128;                      // 64 history rows x K (<= 32) fp32
+constexpr int kXchB = kWaves * 32 * 32 * 4;          // candidate partials [wave][c][k], 32x32 fp32 each
+constexpr int kLogB = 64 * 128;                      // 64 history rows x K (<= 32) fp32; then A in place
 constexpr int kL1B = 4 * 64 * 3 + 4 * kMaxCand;      // his ids | mask words | bias | cand ids
-constexpr int kL0B = 256;
+constexpr int kL0B = 16;                             // CSR offsets (2 ints) of one impression
+constexpr int kPrepB = 2 * 64 * 4;                   // softmax coefficients (mul | add) per history slot
 constexpr int kOffX = kRingB;
 constexpr int kOffLog = kOffX + kXchB;
 constexpr int kOffL1 = kOffLog + 2 * kLogB;
 constexpr int kOffL0 = kOffL1 + 4 * kL1B;
-constexpr int kPrepB = 2 * 64 * 4;                   // softmax coefficients (mul | add) per history slot
-constexpr int kOffPrep = kOffL0 + 4 * kL0B;
-constexpr int kNewsLds = kOffPrep + 2 * kPrepB;
+constexpr int kOffPrep = kOffL0 + 8 * kL0B;
+constexpr int kOffSoft = kOffPrep + 2 * kPrepB;      // cooperative softmax partials [wave][k][max, sum]
+constexpr int kNewsLds = kOffSoft + kWaves * 32 * 2 * 4;
 static_assert(kNewsLds <= kLdsMax, "news_score LDS");
 static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>::NSLOT * NCfg<float>::SLOT == kRingB, "ring");
 
@@ -384,7 +395,7 @@ __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC
   unsigned t;
   if constexpr (Cf::NI == 1) {
     asm volatile(
-        "s_nop 4\n\ts_mov_b32 %0, m0\n\t"
+        "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3" NEWS_CP_STR "\n\t"
         "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %4" NEWS_CP_STR "\n\t"
         "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3" NEWS_CP_STR "\n\t"
@@ -394,7 +405,7 @@ __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC
         : "memory");
   } else {
     asm volatile(
-        "s_nop 4\n\ts_mov_b32 %0, m0\n\t"
+        "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5" NEWS_CP_STR "\n\t"
         "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5" NEWS_CP_STR "\n\t"
         "s_mov_b32 m0, %9\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %6" NEWS_CP_STR "\n\t"
@@ -410,18 +421,20 @@ __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC
   }
 }
 
-template <class T, int ST, bool RAGGED>
+template <class T, int ST, bool RAGGED, int PD>
 __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cf = NCfg<T>;
   constexpr int NI = Cf::NI;
+  constexpr int NS = Cf::NSLOT;
+  static_assert(PD >= 1 && PD <= NS - 1, "prefetch depth");
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
   constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int L = p.L, d = p.d;
   const int nchunk = d >> 6;
-  const int PD = nchunk < Cf::NSLOT - 1 ? nchunk : Cf::NSLOT - 1;   // chunks in flight
+  const bool coop = nchunk >= PD + 1 && nchunk >= 4;      // cooperative softmax one impression ahead
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const char* tabB = static_cast<const char*>(p.table);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   auto cands = [&](int i, int& off, int& cnt) {
     if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
     if constexpr (RAGGED) {
-      const int* o = l0_off(smem, i & 3);
+      const int* o = l0_off(smem, i & 7);
       off = __builtin_amdgcn_readfirstlane(o[0]);
       cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
     } else {
@@ -443,42 +456,43 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   };
 
   // ---- aux DMA jobs (issued after a barrier, before that iteration's row DMAs) ----
-  auto issue_aux = [&](int i0) {         // L0 (CSR offsets) of i0 + 3, L1 of i0 + 2, L2 of i0 + 1
+  auto issue_L0 = [&](int i) {           // CSR offsets of impression i
+    if (RAGGED && wave == 0 && i < n_i && (threadIdx.x & 63) < 2)
+      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kOffL0 + (i & 7) * kL0B);
+  };
+  auto issue_L1 = [&](int i) {           // ids / mask / bias of impression i (needs its L0)
+    if (i >= n_i) return;
     const int lane = threadIdx.x & 63;
-    if (RAGGED && wave == 0 && i0 + 3 < n_i && lane < 2)
-      dma_b32(p.cand_off + imp_b(i0 + 3) + lane, sbase + kOffL0 + ((i0 + 3) & 3) * kL0B);
-    if (i0 + 2 < n_i) {                  // ids / mask / bias of impression i0 + 2 (needs its L0)
-      const int i = i0 + 2;
-      const size_t base = (size_t)imp_b(i) * L + min(lane, L - 1);
-      const unsigned l1 = sbase + kOffL1 + (i & 3) * kL1B;
-      if (wave == 1) {
-        NEWS_CHK(1, p.his_ids + base, 4, p.his_ids, (size_t)p.B * L * 4, l1, 256)
-        dma_b32(p.his_ids + base, l1);
-      } else if (wave == 2) {
-        // the aligned word holding mask byte `base` (the reader picks the byte by address)
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
-        NEWS_CHK(2, reinterpret_cast<const void*>(a), 4, p.mask, (size_t)p.B * L + 3, l1 + 256, 256)
-        dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
-      } else if (wave == 3) {
-        if (p.bias) dma_b32(p.bias + base, l1 + 512);
-      } else if (WITH_CAND && wave >= 4) {   // waves 4..7: candidate ids, 64 per DMA (j >= 0)
-        int off, cnt;
-        cands(i, off, cnt);
-        for (int j = wave - 4; j >= 0 && 64 * j < cnt; j += 4) {
-          const int c = min(64 * j + lane, cnt - 1);
-          NEWS_CHK(3, p.cand_ids + off + c, 4, p.cand_ids, (size_t)(RAGGED ? 1 << 30 : p.B * p.C) * 4, l1 + 768 + 256 * j, 256)
-          dma_b32(p.cand_ids + off + c, l1 + 768 + 256 * j);
-        }
+    const size_t base = (size_t)imp_b(i) * L + min(lane, L - 1);
+    const unsigned l1 = sbase + kOffL1 + (i & 3) * kL1B;
+    if (wave == 1) {
+      NEWS_CHK(1, p.his_ids + base, 4, p.his_ids, (size_t)p.B * L * 4, l1, 256)
+      dma_b32(p.his_ids + base, l1);
+    } else if (wave == 2) {
+      // the aligned word holding mask byte `base` (the reader picks the byte by address)
+      const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
+      NEWS_CHK(2, reinterpret_cast<const void*>(a), 4, p.mask, (size_t)p.B * L + 3, l1 + 256, 256)
+      dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
+    } else if (wave == 3) {
+      if (p.bias) dma_b32(p.bias + base, l1 + 512);
+    } else if (WITH_CAND && wave >= 4) { // waves 4..7: candidate ids, 64 per DMA (j >= 0)
+      int off, cnt;
+      cands(i, off, cnt);
+      for (int j = wave - 4; j >= 0 && 64 * j < cnt; j += 4) {
+        const int c = min(64 * j + lane, cnt - 1);
+        NEWS_CHK(3, p.cand_ids + off + c, 4, p.cand_ids, (size_t)(RAGGED ? 1 << 30 : p.B * p.C) * 4, l1 + 768 + 256 * j, 256)
+        dma_b32(p.cand_ids + off + c, l1 + 768 + 256 * j);
       }
     }
-    if (i0 + 1 >= 0 && i0 + 1 < n_i) {   // logit rows of impression i0 + 1's history (needs its L1)
-      const int i = i0 + 1;
-      const int row = min(8 * wave + (lane >> 3), L - 1);
-      const int piece = min(lane & 7, (p.K >> 2) - 1);
-      const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
-      NEWS_CHK(4, p.logits + (size_t)id * p.K + 4 * piece, 16, p.logits, (size_t)p.n_news * p.K * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
-      dma_b128_c(p.logits + (size_t)id * p.K + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
-    }
+  };
+  auto issue_L2 = [&](int i) {           // logit rows of impression i's history (needs its L1)
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int row = min(8 * wave + (lane >> 3), L - 1);
+    const int piece = min(lane & 7, (p.K >> 2) - 1);
+    const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
+    NEWS_CHK(4, p.logits + (size_t)id * p.K + 4 * piece, 16, p.logits, (size_t)p.n_news * p.K * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
+    dma_b128_c(p.logits + (size_t)id * p.K + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
   };
   // masked-softmax coefficients of impression i (needs its L1): s_l = logit_l * mul_l + add_l with
   // (mul, add) = (1, bias_l) for a click, (0, 1e-30) for a pad slot (model.py:176-180), (0, -inf)
@@ -497,6 +511,59 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     float* pr = reinterpret_cast<float*>(smem + kOffPrep + (i & 1) * kPrepB);
     pr[l] = mul;
     pr[64 + l] = add;
+  };
+  // cooperative softmax over the history (model.py:176-181), one impression ahead: phase 1 — wave w
+  // takes history slots [8w, 8w+8), lane (h, k) four of them: partial (max, Σexp) per interest k;
+  // phase 2 (after a barrier) — merge the 8 partials, write A[l][k] over the logit rows the wave
+  // read (its own rows only: no wave reads another's), bf16 / fp32 as the MFMA operand
+  auto soft_phase = [&](int i, int phase) {
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int k = lane & 31, h = lane >> 5;
+    char* lg = smem + kOffLog + (i & 1) * kLogB;
+    const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    float* part = reinterpret_cast<float*>(smem + kOffSoft);
+    const int l0 = 8 * wave + 4 * h;
+    const float4 mu = *reinterpret_cast<const float4*>(pr + l0);
+    const float4 ad = *reinterpret_cast<const float4*>(pr + 64 + l0);
+    const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
+    float x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = __builtin_fmaf(reinterpret_cast<const float*>(lg + (l0 + j) * 128)[k], m4[j], a4[j]);
+    if (phase == 1) {
+      float m = fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3]));
+      float s = 0.f;
+      if (m != -INFINITY) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += nx_exp<T>(x[j] - m);
+      }
+      const float mo = both_max(m);      // combine the two lane halves
+      const float so = (m == -INFINITY ? 0.f : s * nx_exp<T>(m - mo));
+      const float st = mo == -INFINITY ? 0.f : both_sum(so);
+      if (h == 0) {
+        part[(wave * 32 + k) * 2] = mo;
+        part[(wave * 32 + k) * 2 + 1] = st;
+      }
+    } else {
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) M = fmaxf(M, part[(w * 32 + k) * 2]);
+      float S = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const float mw = part[(w * 32 + k) * 2];
+        if (mw != -INFINITY) S += part[(w * 32 + k) * 2 + 1] * nx_exp<T>(mw - M);
+      }
+      float inv;
+      if constexpr (sizeof(T) == 2) inv = __builtin_amdgcn_rcpf(S); else inv = 1.0f / S;
+      if (k >= p.K) inv = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = nx_exp<T>(x[j] - M) * inv;
+        if constexpr (sizeof(T) == 2) reinterpret_cast<T*>(lg + (l0 + j) * 128)[k] = (T)a;
+        else reinterpret_cast<float*>(lg + (l0 + j) * 128)[k] = a;
+      }
+    }
   };
   // this lane's row offsets (bytes, + its swizzled 16-byte piece) for item (i, pass): the history
   // row (E and proj parts) and the candidate row of each of its NI DMA blocks
@@ -527,8 +594,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
 
   // ---- per-lane LDS read offsets of this wave's operands (fixed for the whole launch) ----
   const int P = wave >> 2, sl = (wave >> 1) & 1, ct = wave & 1;
-  uint32_t trOff[8];                   // bf16: transposed part reads, rows 32 ls + .., [ls][s][u]
+  uint32_t trOff[8];                   // bf16: transposed reads [ls][s][u] of part rows / A rows
   uint32_t cOff[kNQ<T>];               // candidate row 32 ct + pi(r), columns [32 sl + 16 h, +16)
+  uint32_t aOff[4];                    // bf16 coop: A[l][k] rows 16 h + .., transposed reads [s][u]
   {
     const int lane = threadIdx.x & 63;
     const int r = lane & 31, h = lane >> 5;
@@ -543,6 +611,12 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
           const int row = 32 * ls + 16 * (g >> 1) + 8 * (su >> 1) + 4 * (su & 1) + q;
           trOff[4 * ls + su] = row * 128 + ((ch ^ nswz<T>(row)) << 4) + sub;
         }
+      // A stored [l][k] (bf16, row stride 128 B): block rows l, columns k = 16 (g & 1) + 4 pp ..
+#pragma unroll
+      for (int su = 0; su < 4; ++su) {
+        const int row = 16 * (g >> 1) + 8 * (su >> 1) + 4 * (su & 1) + q;
+        aOff[su] = row * 128 + (16 * (g & 1) + 4 * pp) * 2;
+      }
     }
     const int row = 32 * ct + pi_row(r);
     const int ch0 = sizeof(T) == 2 ? 4 * sl + 2 * h : 8 * sl + 4 * h;
@@ -550,74 +624,167 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     for (int q = 0; q < kNQ<T>; ++q) cOff[q] = row * Cf::RB + (((ch0 + q) ^ nswz<T>(row)) << 4);
   }
 
-  // ---- prologue: aux for the first impressions, then the first PD chunks ----
-  if (RAGGED && wave == 0 && (threadIdx.x & 63) < 2)
-    for (int i = 0; i < 3 && i < n_i; ++i)
-      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kOffL0 + i * kL0B);
-  vm_wait_all();
-  raw_barrier();
-  issue_aux(-2);                       // L1 of impression 0 (and L0 of 1, which has landed)
-  vm_wait_all();
-  raw_barrier();
-  issue_aux(-1);                       // L1 of 1, logits of 0
-  prep_softmax(0);
-  vm_wait_all();
-  raw_barrier();
-  uint32_t cH[NI], cC[NI], nH[NI], nC[NI];   // row offsets of the current / next item
-  item_offsets(0, 0, cH, cC);
-  for (int k = 0; k < PD; ++k)
-    if (!(p.abl & 2)) dma_chunk<T>(cH, cC, tabB + k * 64 * sizeof(T), prjB + k * 64 * sizeof(T), sbase + k * Cf::SLOT + wave * 1024);
-
   Frag<T> af[2];                       // attention weights A [K, 64] as two B-operand slabs
-  f32x16 acc = zero16();               // this wave's M / Lg partial, one 32x32 candidate tile
-  int pend_off = -1, pend_cnt = 0;     // a finished pass waiting for S7 (pend_off >= 0)
-  int t = 0;
-
-  auto s7 = [&]() {
-    FRESH_LANE_IDS();
-    const int tct = wave & 1, e0 = 4 * (wave >> 1);
-    const float* X = reinterpret_cast<const float*>(smem + kOffX);
-    const bool kv = r < p.K;
+  // A of impression i -> af: from the A rows written by soft_phase (coop), else computed in-wave
+  auto load_af = [&](int i) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const char* lg = smem + kOffLog + (i & 1) * kLogB;
 #pragma unroll
-    for (int ee = 0; ee < 4; ++ee) {
-      const int e = e0 + ee;
-      const float m = X[((0 + tct) * 16 + e) * 64 + lane] + X[((2 + tct) * 16 + e) * 64 + lane];
-      float sc;
-      if constexpr (WEIGHTED) {
-        const float lg = X[((4 + tct) * 16 + e) * 64 + lane] + X[((6 + tct) * 16 + e) * 64 + lane];
-        const float mx = half_max(kv ? lg : -INFINITY);
-        const float pe = kv ? nx_exp<T>(lg - mx) : 0.f;
-        const float s = half_sum(pe);
-        const float num = half_sum(pe * m);
-        if constexpr (sizeof(T) == 2) sc = num * __builtin_amdgcn_rcpf(s); else sc = num / s;
+    for (int ls = 0; ls < 2; ++ls) {
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int su = 0; su < 4; ++su) {
+          const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds_char*)(lg + 32 * ls * 128 + aOff[su]));
+          const auto w2 = __builtin_bit_cast(uint2, v);
+          af[ls].q[su >> 1][2 * (su & 1)] = w2.x;
+          af[ls].q[su >> 1][2 * (su & 1) + 1] = w2.y;
+        }
       } else {
-        if (p.score_type == MINER_SCORE_MAX) sc = half_max(kv ? m : -INFINITY);
-        else sc = half_sum(kv ? m : 0.f) / (float)p.K;
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          af[ls].q[e >> 2][e & 3] = __float_as_uint(reinterpret_cast<const float*>(lg + (32 * ls + 16 * h + e) * 128)[r]);
       }
-      const int c = 32 * tct + 16 * h + e;
-      if (r == ee && c < pend_cnt) {
-        NEWS_CHK(8, p.scores + pend_off + c, 4, p.scores, (size_t)(RAGGED ? 1 << 30 : p.B * p.C) * 4, 0, 0)
-        p.scores[pend_off + c] = sc;
+    }
+  };
+  auto softmax_inwave = [&](int i) {   // small d: every wave computes A of impression i itself
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
+    const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    float v[32];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int ls = 0; ls < 2; ++ls) {
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int l0 = 32 * ls + 16 * h + 4 * j4;
+        const float4 mu = *reinterpret_cast<const float4*>(pr + l0);
+        const float4 ad = *reinterpret_cast<const float4*>(pr + 64 + l0);
+        const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float s = __builtin_fmaf(lgb[(l0 + u) * 32 + r], m4[u], a4[u]);
+          v[16 * ls + 4 * j4 + u] = s;
+          mx = fmaxf(mx, s);
+        }
+      }
+    }
+    mx = both_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      v[j] = nx_exp<T>(v[j] - mx);     // exp(-inf) = 0 past L
+      sum += v[j];
+    }
+    sum = both_sum(sum);
+    float inv;
+    if constexpr (sizeof(T) == 2) inv = __builtin_amdgcn_rcpf(sum); else inv = 1.0f / sum;
+    if (r >= p.K) inv = 0.f;
+#pragma unroll
+    for (int ls = 0; ls < 2; ++ls) {
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) af[ls].q[m >> 2][m & 3] = pack_bf16x2(v[16 * ls + 2 * m] * inv, v[16 * ls + 2 * m + 1] * inv);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) af[ls].q[e >> 2][e & 3] = __float_as_uint(v[16 * ls + e] * inv);
       }
     }
   };
 
-  // one 64-column chunk of item (ci, cp): wait for its slot, the row DMAs PD chunks ahead, the X /
-  // mui slab and the candidate product. `mode`: 1 X, 2 candidate product, 4 mui out
-  auto chunk = [&](int ci, int cc, int mode, int ni, int np) {
-    // row DMAs PD chunks ahead (into the next item near the end of this one)
-    {
-      const int ic = cc + PD;
-      if (ic == nchunk) item_offsets(ni, np, nH, nC);
-      const bool nx = ic >= nchunk;
-      const int ch = nx ? ic - nchunk : ic;
-      if (!(p.abl & 2))
-        dma_chunk<T>(nx ? nH : cH, nx ? nC : cC, tabB + ch * 64 * sizeof(T), prjB + ch * 64 * sizeof(T),
-                     sbase + ((t + PD) % Cf::NSLOT) * Cf::SLOT + wave * 1024);
+  // ---- prologue: aux for the first impressions, A of impression 0, then the first PD chunks ----
+  for (int i = 0; i < 4; ++i) issue_L0(i);
+  vm_wait_all();
+  raw_barrier();
+  issue_L1(0); issue_L1(1); issue_L1(2);
+  vm_wait_all();
+  raw_barrier();
+  issue_L2(0); issue_L2(1);
+  prep_softmax(0); prep_softmax(1);
+  vm_wait_all();
+  raw_barrier();
+  if (coop) {
+    soft_phase(0, 1);
+    raw_barrier();
+    soft_phase(0, 2);
+    raw_barrier();
+  }
+  uint32_t cH[NI], cC[NI], nH[NI], nC[NI];   // row offsets of the current / next item
+  item_offsets(0, 0, cH, cC);
+#pragma unroll
+  for (int k = 0; k < PD; ++k)
+    dma_chunk<T>(cH, cC, tabB + k * 64 * sizeof(T), prjB + k * 64 * sizeof(T), sbase + k * Cf::SLOT + wave * 1024);
+
+  f32x16 acc = zero16();               // this wave's M / Lg partial, one 32x32 candidate tile
+  int pend_off = -1, pend_cnt = 0;     // a finished pass waiting for S7 (pend_off >= 0)
+  int t = 0;
+
+  // S7 (model.py:128-136, :213-214) on waves 0..3: wave w takes candidates [16 w, 16 w + 16) of the
+  // pass, lane (kq, c) = (lane >> 4, lane & 15) interests [8 kq, 8 kq + 8); partials of the 8 waves
+  // are summed here (M: waves ct, 2+ct; Lg: 4+ct, 6+ct), the 4 lane rows combined by permlanes
+  auto s7 = [&]() {
+    if (wave >= 4) return;
+    const int lane = threadIdx.x & 63;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int c = 16 * wave + cl;              // candidate of the pass
+    const int tct = c >> 5, cr = c & 31;       // c-tile, row in the tile
+    const float* X = reinterpret_cast<const float*>(smem + kOffX);
+    const int sw = (cr >> 1) & 31;
+    float lg[8], m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * kq + j;
+      const int o = cr * 32 + (k ^ sw);
+      m[j] = X[(tct) * 1024 + o] + X[(2 + tct) * 1024 + o];
+      if constexpr (WEIGHTED) lg[j] = X[(4 + tct) * 1024 + o] + X[(6 + tct) * 1024 + o];
     }
+    float sc;
+    if constexpr (WEIGHTED) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, lg[j]);
+      mx = rows4_max(mx);
+      float s = 0.f, num = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (8 * kq + j < p.K) {
+          const float pe = nx_exp<T>(lg[j] - mx);
+          s += pe;
+          num = __builtin_fmaf(pe, m[j], num);
+        }
+      }
+      s = rows4_sum(s);
+      num = rows4_sum(num);
+      if constexpr (sizeof(T) == 2) sc = num * __builtin_amdgcn_rcpf(s); else sc = num / s;
+    } else {
+      if (p.score_type == MINER_SCORE_MAX) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, m[j]);
+        sc = rows4_max(mx);
+      } else {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) s += m[j];
+        sc = rows4_sum(s) / (float)p.K;
+      }
+    }
+    if (kq == 0 && c < pend_cnt) {
+      NEWS_CHK(8, p.scores + pend_off + c, 4, p.scores, (size_t)(RAGGED ? 1 << 30 : p.B * p.C) * 4, 0, 0)
+      p.scores[pend_off + c] = sc;
+    }
+  };
+
+  // one 64-column chunk: the row DMAs of chunk `ich` of the item whose offsets are (iH, iC), PD
+  // chunks ahead, then the X / mui slab and the candidate product of this chunk.
+  // `mode`: 1 X, 2 candidate product, 4 mui out
+  auto chunk = [&](int ci, int cc, int mode, const uint32_t* iH, const uint32_t* iC, int ich) {
+    dma_chunk<T>(iH, iC, tabB + ich * 64 * sizeof(T), prjB + ich * 64 * sizeof(T),
+                 sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024);
     if (mode & 1) {
       FRESH_LANE_IDS();
-      const char* slot = smem + (t % Cf::NSLOT) * Cf::SLOT;
+      const char* slot = smem + (t & (NS - 1)) * Cf::SLOT;
       const char* part = slot + P * Cf::PART;
       f32x16 ax = zero16();
 #pragma unroll
@@ -654,7 +821,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   };
   auto wait_slot = [&]() {
     // slot t landed (this wave's DMAs: all but the PD-1 younger chunks), then for every wave
-    if (PD >= 3) vm_wait<3 * NI * 2>(); else if (PD == 2) vm_wait<3 * NI>(); else vm_wait<0>();
+    vm_wait<3 * NI * (PD - 1)>();
     raw_barrier();
   };
 
@@ -667,77 +834,61 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       const bool need_c = WITH_CAND && (ct == 0 || cntp > 32) && (P == 0 || WEIGHTED);
       const bool need_mui = P == 0 && p.mui_out != nullptr && cp == 0 && ct == 0;
       const bool need_x = (P == 0) ? (WITH_CAND || need_mui) : WEIGHTED;
-      const int mode = (p.abl & 1) ? 0 : ((need_x && (need_c || need_mui)) ? 1 : 0) | (need_c ? 2 : 0) | (need_mui ? 4 : 0);
+      const int mode = ((need_x && (need_c || need_mui)) ? 1 : 0) | (need_c ? 2 : 0) | (need_mui ? 4 : 0);
       // the item after this one, for the DMAs that run ahead into it
       const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
-
-      // ---- first chunk of the item, with the per-item work ----
-      wait_slot();
-      if (cp == 0) issue_aux(ci);
-      const bool did_s7 = WITH_CAND && pend_off >= 0;
-      if (did_s7) s7();
-      pend_off = -1;
-      if (cp == 0) {
-        prep_softmax(ci + 1);
-        // ---- attention weights of impression ci: softmax over the history (model.py:176-181) ----
-        FRESH_LANE_IDS();
-        const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (ci & 1) * kLogB);
-        const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (ci & 1) * kPrepB);
-        float v[32];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int ls = 0; ls < 2; ++ls) {
-#pragma unroll
-          for (int j4 = 0; j4 < 4; ++j4) {
-            const int l0 = 32 * ls + 16 * h + 4 * j4;
-            const float4 mu = *reinterpret_cast<const float4*>(pr + l0);
-            const float4 ad = *reinterpret_cast<const float4*>(pr + 64 + l0);
-            const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const float s = __builtin_fmaf(lgb[(l0 + u) * 32 + r], m4[u], a4[u]);
-              v[16 * ls + 4 * j4 + u] = s;
-              mx = fmaxf(mx, s);
+      bool did_s7 = false;
+      // per-item work riding on the first chunks of the item
+      auto extras = [&](int cc) {
+        if (cc == 0) {
+          did_s7 = WITH_CAND && pend_off >= 0;
+          if (did_s7) s7();
+          pend_off = -1;
+          if (cp == 0) {
+            if (coop) {
+              load_af(ci);
+            } else {
+              softmax_inwave(ci);
+              raw_barrier();           // every wave has read impression ci's logit rows
+              issue_L2(ci + 2);
             }
+            issue_L0(ci + 4);
+            issue_L1(ci + 3);
+            prep_softmax(ci + 2);
+          }
+          acc = zero16();
+        } else if (coop && cp == 0) {
+          if (cc == 1) {
+            issue_L2(ci + 2);          // into the rows A of ci was read from (free since the barrier)
+            soft_phase(ci + 1, 1);
+          } else if (cc == 2) {
+            soft_phase(ci + 1, 2);
           }
         }
-        mx = both_max(mx);
-        float sum = 0.f;
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-          v[j] = nx_exp<T>(v[j] - mx);     // exp(-inf) = 0 past L
-          sum += v[j];
-        }
-        sum = both_sum(sum);
-        float inv;
-        if constexpr (sizeof(T) == 2) inv = __builtin_amdgcn_rcpf(sum); else inv = 1.0f / sum;
-        if (r >= p.K) inv = 0.f;
-#pragma unroll
-        for (int ls = 0; ls < 2; ++ls) {
-          if constexpr (sizeof(T) == 2) {
-#pragma unroll
-            for (int m = 0; m < 8; ++m) af[ls].q[m >> 2][m & 3] = pack_bf16x2(v[16 * ls + 2 * m] * inv, v[16 * ls + 2 * m + 1] * inv);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) af[ls].q[e >> 2][e & 3] = __float_as_uint(v[16 * ls + e] * inv);
-          }
-        }
-      }
-      acc = zero16();
-      chunk(ci, 0, mode, ni, np);
-      ++t;
-      // ---- the other chunks ----
-      for (int cc = 1; cc < nchunk; ++cc, ++t) {
+      };
+      int cc = 0;
+      for (; cc < nchunk - PD; ++cc, ++t) {
         wait_slot();
-        chunk(ci, cc, mode, ni, np);
+        extras(cc);
+        chunk(ci, cc, mode, cH, cC, cc + PD);
       }
-      // pass done: partials -> LDS, S7 at the next item's first chunk
+      item_offsets(ni, np, nH, nC);
+      for (; cc < nchunk; ++cc, ++t) {
+        wait_slot();
+        extras(cc);
+        chunk(ci, cc, mode, nH, nC, cc + PD - nchunk);
+      }
+      // pass done: partials -> LDS ([wave][c][k ^ swizzle]), S7 at the next item's first chunk
       if (nchunk == 1 && did_s7) raw_barrier();
       {
         const int lane = threadIdx.x & 63;
-        float* dst = reinterpret_cast<float*>(smem + kOffX) + (wave * 16) * 64 + lane;
+        const int r = lane & 31, h = lane >> 5;
+        float* dst = reinterpret_cast<float*>(smem + kOffX) + wave * 1024;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) dst[e * 64] = acc[e];
+        for (int e = 0; e < 16; ++e) {
+          const int cr = 16 * h + e;
+          dst[cr * 32 + (r ^ ((cr >> 1) & 31))] = acc[e];
+        }
       }
       pend_off = c_off + 64 * cp;
       pend_cnt = cntp;
@@ -808,11 +959,21 @@ template <class T>
 int launch_score(void* stream, const NsParams& prm) {
   void (*kern)(NsParams) = nullptr;
   const bool rg = prm.cand_off != nullptr;
-  switch (prm.score_type) {
-    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true> : news_score<T, MINER_SCORE_WEIGHTED, false>; break;
-    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false>; break;
-    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true> : news_score<T, MINER_SCORE_MAX, false>; break;
+  const int nchunk = prm.d >> 6;
+  constexpr int maxpd = NCfg<T>::NSLOT - 1;
+  const int pd = nchunk < maxpd ? nchunk : maxpd;
+#define NEWS_PICK(PDV)                                                                                   \
+  switch (prm.score_type) {                                                                            \
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true, PDV> : news_score<T, MINER_SCORE_WEIGHTED, false, PDV>; break; \
+    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false, PDV>; break;                   \
+    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true, PDV> : news_score<T, MINER_SCORE_MAX, false, PDV>; break; \
   }
+  if constexpr (maxpd >= 3) {
+    if (pd == 3) { NEWS_PICK(3) } else if (pd == 2) { NEWS_PICK(2) } else { NEWS_PICK(1) }
+  } else {
+    NEWS_PICK(1)
+  }
+#undef NEWS_PICK
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kNewsLds);
   if (e != hipSuccess) return (int)e;
   int grid = num_cus();
