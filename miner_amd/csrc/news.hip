@@ -294,14 +294,15 @@ __device__ __forceinline__ bool dbg_ok(int kind, const void* a, size_t n, const 
 #define NEWS_CHK(kind, a, n, lo, range, lds, lds_n)
 #endif
 
-template <class T> struct NCfg {
-  static constexpr int RB = 64 * (int)sizeof(T);     // bytes of one row of a 64-column chunk
+template <class T, int CW = 64> struct NCfg {   // CW: columns per chunk (64, or 128 for 16-bit)
+  static constexpr int RB = CW * (int)sizeof(T);     // bytes of one row of a chunk
   static constexpr int PART = 64 * RB;               // 64 rows: E[his] | proj[his] | Cand
   static constexpr int SLOT = 3 * PART;
-  static constexpr int NSLOT = sizeof(T) == 2 ? 4 : 2;
+  static constexpr int NSLOT = (sizeof(T) == 2 && CW == 64) ? 4 : 2;
   static constexpr int NI = RB / 128;                // DMA instructions per part per wave
   static constexpr int RPI = 1024 / RB;              // rows per DMA instruction
   static constexpr int PPR = RB / 16;                // 16-byte pieces per row
+  static constexpr int NSLAB = CW / 32;              // 32-column slabs per chunk
 };
 
 // LDS carve (bytes): [ring | xchg | logit blocks x2 | aux L1 x4 | aux L0 x4]
@@ -319,16 +320,16 @@ constexpr int kOffPrep = kOffL0 + 8 * kL0B;
 constexpr int kOffSoft = kOffPrep + 2 * kPrepB;      // cooperative softmax partials [wave][k][max, sum]
 constexpr int kNewsLds = kOffSoft + kWaves * 32 * 2 * 4;
 static_assert(kNewsLds <= kLdsMax, "news_score LDS");
-static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>::NSLOT * NCfg<float>::SLOT == kRingB, "ring");
+static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>::NSLOT * NCfg<float>::SLOT == kRingB &&
+              NCfg<__bf16, 128>::NSLOT * NCfg<__bf16, 128>::SLOT == kRingB, "ring");
 
 // chunk swizzle of a slot row: bf16 (8 chunks per row, 2 rows per 256-byte bank row): rows 4q..4q+3
 // of a transposed read hit disjoint banks and 16 rows of a ds_read_b128 group distinct slots;
 // fp32 (16 chunks per row): row & 15
-template <class T> __device__ __forceinline__ int nswz(int row) {
-  if constexpr (sizeof(T) == 2) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+template <class T, int CW = 64> __device__ __forceinline__ int nswz(int row) {
+  if constexpr (NCfg<T, CW>::PPR == 8) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
   else return row & 15;
 }
-
 // A-operand fragment of a part's transpose: rows = columns 32 sl + pi(r) of the chunk, contraction
 // over the 32 part rows 32 ls .. 32 ls + 31 (bf16: ds_read_b64_tr_b16)
 template <class T>
@@ -388,10 +389,10 @@ __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpre
 #else
 #define NEWS_CP_STR ""
 #endif
-template <class T>
+template <class T, int CW>
 __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC, const char* bE, const char* bY,
                                           unsigned mE) {
-  using Cf = NCfg<T>;
+  using Cf = NCfg<T, CW>;
   unsigned t;
   if constexpr (Cf::NI == 1) {
     asm volatile(
@@ -421,10 +422,12 @@ __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC
   }
 }
 
-template <class T, int ST, bool RAGGED, int PD>
+template <class T, int ST, bool RAGGED, int PD, int CW>
 __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using Cf = NCfg<T>;
+  using Cf = NCfg<T, CW>;
+  constexpr int NSLAB = Cf::NSLAB;
+  constexpr int NT = NSLAB == 4 ? 2 : 1;      // candidate tiles per wave
   constexpr int NI = Cf::NI;
   constexpr int NS = Cf::NSLOT;
   static_assert(PD >= 1 && PD <= NS - 1, "prefetch depth");
@@ -433,8 +436,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int L = p.L, d = p.d;
-  const int nchunk = d >> 6;
-  const bool coop = nchunk >= PD + 1 && nchunk >= 4;      // cooperative softmax one impression ahead
+  const int nchunk = d / CW;
+  // cooperative softmax one impression ahead (always for 128-column chunks: the host picks them for d >= 512)
+  const bool coop = CW == 128 || (nchunk >= PD + 1 && nchunk >= 4);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const char* tabB = static_cast<const char*>(p.table);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
 #pragma unroll
     for (int jj = 0; jj < NI; ++jj) {
       const int rowp = (wave + 8 * jj) * Cf::RPI + lane / Cf::PPR;
-      const uint32_t poff = (uint32_t)(((lane % Cf::PPR) ^ nswz<T>(rowp)) << 4);
+      const uint32_t poff = (uint32_t)(((lane % Cf::PPR) ^ nswz<T, CW>(rowp)) << 4);
       int h = 0, c = 0;
       if (live) {
         h = hid[min(rowp, L - 1)];
@@ -593,9 +597,14 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   };
 
   // ---- per-lane LDS read offsets of this wave's operands (fixed for the whole launch) ----
-  const int P = wave >> 2, sl = (wave >> 1) & 1, ct = wave & 1;
-  uint32_t trOff[8];                   // bf16: transposed reads [ls][s][u] of part rows / A rows
-  uint32_t cOff[kNQ<T>];               // candidate row 32 ct + pi(r), columns [32 sl + 16 h, +16)
+  // wave roles: P = path (0: E -> mui -> M, 1: proj -> X -> Lg), sl = slab of the chunk, ct = candidate
+  // tile (64-column chunks: 2 slabs x 2 tiles, the X slab computed by both tile waves; 128-column
+  // chunks: 4 slabs, each wave both tiles). Waves w and w+4 share a SIMD: one of each path.
+  const int P = wave >> 2;
+  const int sl = NSLAB == 4 ? (wave & 3) : ((wave >> 1) & 1);
+  const int ct = NSLAB == 4 ? 0 : (wave & 1);
+  uint32_t trOff[8];                   // bf16: transposed reads [ls][s][u] of part rows
+  uint32_t cOff[NT][kNQ<T>];           // candidate rows 32 tile + pi(r), columns [32 sl + 16 h, +16)
   uint32_t aOff[4];                    // bf16 coop: A[l][k] rows 16 h + .., transposed reads [s][u]
   {
     const int lane = threadIdx.x & 63;
@@ -609,7 +618,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
 #pragma unroll
         for (int su = 0; su < 4; ++su) {
           const int row = 32 * ls + 16 * (g >> 1) + 8 * (su >> 1) + 4 * (su & 1) + q;
-          trOff[4 * ls + su] = row * 128 + ((ch ^ nswz<T>(row)) << 4) + sub;
+          trOff[4 * ls + su] = row * Cf::RB + ((ch ^ nswz<T, CW>(row)) << 4) + sub;
         }
       // A stored [l][k] (bf16, row stride 128 B): block rows l, columns k = 16 (g & 1) + 4 pp ..
 #pragma unroll
@@ -618,10 +627,13 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         aOff[su] = row * 128 + (16 * (g & 1) + 4 * pp) * 2;
       }
     }
-    const int row = 32 * ct + pi_row(r);
-    const int ch0 = sizeof(T) == 2 ? 4 * sl + 2 * h : 8 * sl + 4 * h;
 #pragma unroll
-    for (int q = 0; q < kNQ<T>; ++q) cOff[q] = row * Cf::RB + (((ch0 + q) ^ nswz<T>(row)) << 4);
+    for (int tl = 0; tl < NT; ++tl) {
+      const int row = 32 * (NT == 2 ? tl : ct) + pi_row(r);
+      const int ch0 = sizeof(T) == 2 ? 4 * sl + 2 * h : 8 * sl + 4 * h;
+#pragma unroll
+      for (int q = 0; q < kNQ<T>; ++q) cOff[tl][q] = row * Cf::RB + (((ch0 + q) ^ nswz<T, CW>(row)) << 4);
+    }
   }
 
   Frag<T> af[2];                       // attention weights A [K, 64] as two B-operand slabs
@@ -714,9 +726,11 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   item_offsets(0, 0, cH, cC);
 #pragma unroll
   for (int k = 0; k < PD; ++k)
-    dma_chunk<T>(cH, cC, tabB + k * 64 * sizeof(T), prjB + k * 64 * sizeof(T), sbase + k * Cf::SLOT + wave * 1024);
+    dma_chunk<T, CW>(cH, cC, tabB + k * CW * sizeof(T), prjB + k * CW * sizeof(T), sbase + k * Cf::SLOT + wave * 1024);
 
-  f32x16 acc = zero16();               // this wave's M / Lg partial, one 32x32 candidate tile
+  f32x16 acc[NT];                      // this wave's M / Lg partials, 32x32 candidate tiles
+#pragma unroll
+  for (int tl = 0; tl < NT; ++tl) acc[tl] = zero16();
   int pend_off = -1, pend_cnt = 0;     // a finished pass waiting for S7 (pend_off >= 0)
   int t = 0;
 
@@ -779,9 +793,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   // one 64-column chunk: the row DMAs of chunk `ich` of the item whose offsets are (iH, iC), PD
   // chunks ahead, then the X / mui slab and the candidate product of this chunk.
   // `mode`: 1 X, 2 candidate product, 4 mui out
-  auto chunk = [&](int ci, int cc, int mode, const uint32_t* iH, const uint32_t* iC, int ich) {
-    dma_chunk<T>(iH, iC, tabB + ich * 64 * sizeof(T), prjB + ich * 64 * sizeof(T),
-                 sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024);
+  auto chunk = [&](int ci, int cc, int mode, int ncand, const uint32_t* iH, const uint32_t* iC, int ich) {
+    dma_chunk<T, CW>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
+                     sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024);
     if (mode & 1) {
       FRESH_LANE_IDS();
       const char* slot = smem + (t & (NS - 1)) * Cf::SLOT;
@@ -804,18 +818,24 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         mma_slab(ax, ef, af[ls]);
       }
       if ((mode & 4) && r < p.K) {
-        float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + r) * d + 64 * cc + 32 * sl + 16 * h;
+        float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + r) * d + CW * cc + 32 * sl + 16 * h;
 #pragma unroll
         for (int e = 0; e < 16; e += 4) *reinterpret_cast<float4*>(dst + e) = make_float4(ax[e], ax[e + 1], ax[e + 2], ax[e + 3]);
       }
       if (mode & 2) {
         if (WEIGHTED && P == 1) gelu_tile<T>(ax);
-        Frag<T> xf, cf;
+        Frag<T> xf;
         acc_to_frag<T>(xf, ax);
         const char* cpart = slot + 2 * Cf::PART;
 #pragma unroll
-        for (int q = 0; q < kNQ<T>; ++q) cf.q[q] = lds_u32x4(cpart + cOff[q]);
-        mma_slab(acc, cf, xf);
+        for (int tl = 0; tl < NT; ++tl) {
+          if (tl == 0 || ncand > 32) {
+            Frag<T> cf;
+#pragma unroll
+            for (int q = 0; q < kNQ<T>; ++q) cf.q[q] = lds_u32x4(cpart + cOff[tl][q]);
+            mma_slab(acc[tl], cf, xf);
+          }
+        }
       }
     }
   };
@@ -832,7 +852,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     for (int cp = 0; cp < cn; ++cp) {
       const int cntp = min(64, c_cnt - 64 * cp);
       const bool need_c = WITH_CAND && (ct == 0 || cntp > 32) && (P == 0 || WEIGHTED);
-      const bool need_mui = P == 0 && p.mui_out != nullptr && cp == 0 && ct == 0;
+      const bool need_mui = P == 0 && p.mui_out != nullptr && cp == 0 && ct == 0;   // NSLAB 4: ct == 0
       const bool need_x = (P == 0) ? (WITH_CAND || need_mui) : WEIGHTED;
       const int mode = ((need_x && (need_c || need_mui)) ? 1 : 0) | (need_c ? 2 : 0) | (need_mui ? 4 : 0);
       // the item after this one, for the DMAs that run ahead into it
@@ -847,7 +867,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
           if (cp == 0) {
             if (coop) {
               load_af(ci);
-            } else {
+            } else if constexpr (CW == 64) {
               softmax_inwave(ci);
               raw_barrier();           // every wave has read impression ci's logit rows
               issue_L2(ci + 2);
@@ -856,7 +876,8 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
             issue_L1(ci + 3);
             prep_softmax(ci + 2);
           }
-          acc = zero16();
+#pragma unroll
+          for (int tl = 0; tl < NT; ++tl) acc[tl] = zero16();
         } else if (coop && cp == 0) {
           if (cc == 1) {
             issue_L2(ci + 2);          // into the rows A of ci was read from (free since the barrier)
@@ -870,24 +891,49 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       for (; cc < nchunk - PD; ++cc, ++t) {
         wait_slot();
         extras(cc);
-        chunk(ci, cc, mode, cH, cC, cc + PD);
+        chunk(ci, cc, mode, cntp, cH, cC, cc + PD);
       }
       item_offsets(ni, np, nH, nC);
       for (; cc < nchunk; ++cc, ++t) {
         wait_slot();
         extras(cc);
-        chunk(ci, cc, mode, nH, nC, cc + PD - nchunk);
+        chunk(ci, cc, mode, cntp, nH, nC, cc + PD - nchunk);
       }
-      // pass done: partials -> LDS ([wave][c][k ^ swizzle]), S7 at the next item's first chunk
+      // pass done: partials -> LDS blocks [c][k ^ swizzle] (block = 4P + 2 sl + tile for the two
+      // slab halves that survive), S7 at the next item's first chunk
       if (nchunk == 1 && did_s7) raw_barrier();
       {
         const int lane = threadIdx.x & 63;
         const int r = lane & 31, h = lane >> 5;
-        float* dst = reinterpret_cast<float*>(smem + kOffX) + wave * 1024;
+        float* X = reinterpret_cast<float*>(smem + kOffX);
+        auto put = [&](int blk, const f32x16& a) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int cr = 16 * h + e;
-          dst[cr * 32 + (r ^ ((cr >> 1) & 31))] = acc[e];
+          for (int e = 0; e < 16; ++e) {
+            const int cr = 16 * h + e;
+            X[blk * 1024 + cr * 32 + (r ^ ((cr >> 1) & 31))] = a[e];
+          }
+        };
+        if constexpr (NSLAB == 4) {
+          // slabs 2, 3 hand their partials to slabs 0, 1 (same path), which add and publish
+          if (sl >= 2) {
+#pragma unroll
+            for (int tl = 0; tl < 2; ++tl) put(4 * P + 2 * (sl - 2) + tl, acc[tl]);
+          }
+          raw_barrier();
+          if (sl < 2) {
+#pragma unroll
+            for (int tl = 0; tl < 2; ++tl) {
+              const int blk = 4 * P + 2 * sl + tl;
+#pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                const int cr = 16 * h + e;
+                acc[tl][e] += X[blk * 1024 + cr * 32 + (r ^ ((cr >> 1) & 31))];
+              }
+              put(blk, acc[tl]);
+            }
+          }
+        } else {
+          put(wave, acc[0]);
         }
       }
       pend_off = c_off + 64 * cp;
@@ -959,19 +1005,25 @@ template <class T>
 int launch_score(void* stream, const NsParams& prm) {
   void (*kern)(NsParams) = nullptr;
   const bool rg = prm.cand_off != nullptr;
-  const int nchunk = prm.d >> 6;
-  constexpr int maxpd = NCfg<T>::NSLOT - 1;
-  const int pd = nchunk < maxpd ? nchunk : maxpd;
-#define NEWS_PICK(PDV)                                                                                   \
+#define NEWS_PICK(PDV, CWV)                                                                              \
   switch (prm.score_type) {                                                                            \
-    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true, PDV> : news_score<T, MINER_SCORE_WEIGHTED, false, PDV>; break; \
-    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false, PDV>; break;                   \
-    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true, PDV> : news_score<T, MINER_SCORE_MAX, false, PDV>; break; \
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true, PDV, CWV> : news_score<T, MINER_SCORE_WEIGHTED, false, PDV, CWV>; break; \
+    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false, PDV, CWV>; break;                   \
+    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true, PDV, CWV> : news_score<T, MINER_SCORE_MAX, false, PDV, CWV>; break; \
   }
-  if constexpr (maxpd >= 3) {
-    if (pd == 3) { NEWS_PICK(3) } else if (pd == 2) { NEWS_PICK(2) } else { NEWS_PICK(1) }
+  if constexpr (sizeof(T) == 2) {
+    const int nchunk = prm.d >> 6;
+    if (prm.d % 128 == 0 && prm.d >= 512 && !getenv("MINER_NEWS_CW64")) {
+      NEWS_PICK(1, 128)                // 128-column chunks, double-buffered
+    } else if (nchunk >= 3) {
+      NEWS_PICK(3, 64)
+    } else if (nchunk == 2) {
+      NEWS_PICK(2, 64)
+    } else {
+      NEWS_PICK(1, 64)
+    }
   } else {
-    NEWS_PICK(1)
+    NEWS_PICK(1, 64)
   }
 #undef NEWS_PICK
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kNewsLds);
