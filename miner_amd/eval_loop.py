@@ -3,8 +3,11 @@
 
 The reference builds one sample per (impression, candidate) and runs the whole Miner per sample
 (reader.py:376-379), then groups sigmoid predictions by impression id in Python. Here the news
-encoder output is a device table computed once, each rank scores its contiguous shard of
-impressions with ``ops.score_gather`` in large chunks, and the evaluation stays on the device
+encoder output is a device table computed once, its per-news products are computed once
+(``news.precompute``: tanh(W1 e)·Qᵀ and W2 e), each rank scores its contiguous
+shard of impressions with ``news.score`` in large chunks (``ops.score_gather``, the fused kernel
+with the weights per impression, where the news path's limits do not hold), and the evaluation
+stays on the device
 (``metrics.DeviceEvaluator``); the eval loss keeps the reference's per-batch semantics
 (``evaluation.eval_loss_partials``). Under torchrun every rank returns the same (loss, scores).
 
@@ -26,7 +29,7 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from . import distributed, evaluation, metrics, ops, synthetic
+from . import distributed, evaluation, metrics, news, ops, synthetic
 
 log = logging.getLogger("miner_amd.eval")
 
@@ -34,24 +37,36 @@ log = logging.getLogger("miner_amd.eval")
 def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.Behaviors", metric_names: List[str],
              *, score_type: str = "weighted", evaluation_info=("metrics", "loss"), first_sample: int = 0,
              total_samples: Optional[int] = None, eval_batch_size: int = 32, chunk: int = 32768,
-             save_result: bool = False, path: str = None) -> Tuple[Optional[float], Optional[Dict[str, float]]]:
+             save_result: bool = False, path: str = None,
+             scorer: str = "auto") -> Tuple[Optional[float], Optional[Dict[str, float]]]:
     """Trainer._eval (trainer.py:263-300) for this rank's impressions ``beh`` (a contiguous id range).
 
     ``first_sample`` / ``total_samples``: global index of this shard's first (impression,
     candidate) sample and the total over all ranks — the eval loss's batch partition
-    (eval_batch_size, config/eval_miner.txt:19) is global.
+    (eval_batch_size, config/eval_miner.txt:19) is global. ``scorer``: "news" (per-news precompute +
+    gather-stream kernel), "gather" (fused kernel, weights per impression) or "auto" (news where
+    supported).
     """
     ev = metrics.DeviceEvaluator()
     want_loss = "loss" in evaluation_info
     partial = torch.zeros(2, dtype=torch.float64, device=table.device)
     offs = beh.cand_offsets.to(torch.int64)
     total_samples = int(offs[-1]) if total_samples is None else total_samples
+    L, d = beh.his_ids.shape[1], table.shape[1]
+    max_c = int((offs[1:] - offs[:-1]).max()) if beh.n else 0
+    use_news = scorer == "news" or (scorer == "auto" and news.supported(table.dtype, L, d, packed.Dc, packed.K)
+                                    and max_c <= news.MAX_CAND)
+    nt = news.precompute(table, packed, with_proj=score_type == "weighted") if use_news else None
     for s in range(0, beh.n, chunk):
         e = min(s + chunk, beh.n)
         o0, o1 = int(offs[s]), int(offs[e])
         c_off = (offs[s:e + 1] - o0).to(torch.int32)
-        out = ops.score_gather(table, beh.his_ids[s:e], beh.his_mask[s:e], beh.cand_ids[o0:o1], packed,
-                               score_type=score_type, cand_offsets=c_off, return_user=want_loss, validate=False)
+        if use_news:
+            out = news.score(nt, beh.his_ids[s:e], beh.his_mask[s:e], beh.cand_ids[o0:o1], score_type=score_type,
+                             cand_offsets=c_off, return_user=want_loss, validate=False)
+        else:
+            out = ops.score_gather(table, beh.his_ids[s:e], beh.his_mask[s:e], beh.cand_ids[o0:o1], packed,
+                                   score_type=score_type, cand_offsets=c_off, return_user=want_loss, validate=False)
         scores, mui = out if want_loss else (out, None)
         lab = beh.labels[o0:o1]
         if "metrics" in evaluation_info:

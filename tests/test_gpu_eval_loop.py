@@ -25,10 +25,11 @@ def _setup(device):
     return table, W1, Q, W2
 
 
-def test_eval_loop_matches_oracle():
+@pytest.mark.parametrize("scorer", ["news", "gather"])
+def test_eval_loop_matches_oracle(scorer):
     table, W1, Q, W2 = _setup(DEV)
     beh = synthetic.behaviors(5, 0, CFG["n"], L=CFG["L"], n_news=CFG["n_news"], ragged=CFG["ragged"], device=DEV)
-    loss, scores = eval_loop.evaluate(ops.pack_weights(W1, Q, W2), table, beh, METRICS, chunk=256)
+    loss, scores = eval_loop.evaluate(ops.pack_weights(W1, Q, W2), table, beh, METRICS, chunk=256, scorer=scorer)
     # oracle: reference op order on the gathered rows, one impression at a time (ragged)
     t, w1, q, w2 = table.cpu(), W1.cpu(), Q.cpu(), W2.cpu()
     offs = beh.cand_offsets.cpu().numpy()
