@@ -300,6 +300,54 @@ def dense_kernel_line(dev, B=32768, steps=5):
             "frac_bf16_peak": round(tf / PEAK_BF16_TFLOPS, 4)}
 
 
+def auc_parity(nt16, batch, table, W1, Q, W2, dev, n_imp=2048):
+    """The metric's "AUC parity vs ref", on a bounded sample of the timed batch (part of the CPU
+    baseline leg): scores of the reference CPU path (the oracle: model.py:113-216 as the same torch
+    fp32 ops on the host) vs the GPU news path in its fp32 parity mode and in bf16, then the
+    reference's metrics (evaluation.py:36-84, via the GPU metrics kernel) over one set of labels:
+    Bernoulli(sigmoid(2·z)) of the reference's z-scored scores, with >= 1 click and >= 1 non-click per
+    impression (reader.py:374)."""
+    try:
+        from miner_amd import metrics, news, ops
+        from oracle import miner_oracle as orc
+        hid, mask, cid = [x[:n_imp] for x in batch]
+        t32 = table.float()
+        nt32 = news.precompute(t32, ops.pack_weights(W1, Q, W2, dtype=torch.float32))
+        s32 = news.score(nt32, hid, mask, cid, validate=False)
+        s16 = news.score(nt16, hid, mask, cid, validate=False)
+        T = t32.cpu()
+        h, c = hid.cpu().long(), cid.cpu().long()
+        with torch.no_grad():
+            _, ref = orc.score_torch(T[h], mask.cpu(), T[c], W1.cpu(), Q.cpu(), W2.cpu())
+        g = torch.Generator().manual_seed(36)
+        z = (ref - ref.mean()) / ref.std()
+        lab = (torch.rand(ref.shape, generator=g) < torch.sigmoid(2.0 * z)).to(torch.uint8)
+        rows = torch.arange(ref.shape[0])
+        lab[rows, ref.argmax(1)] = 1
+        lab[rows, ref.argmin(1)] = 0
+        labd = lab.reshape(-1).to(dev)
+        offs = torch.arange(0, (ref.shape[0] + 1) * C, C, dtype=torch.int32, device=dev)
+        names = ["auc", "group_auc", "mrr", "ndcg@5", "ndcg@10"]
+
+        def mets(s):
+            return metrics.compute_metrics(torch.sigmoid(s.float().reshape(-1).to(dev)), labd, offs, names)
+
+        mr, m32, m16 = mets(ref), mets(s32), mets(s16)
+        ok, worst = orc.parity_ok(s32.cpu().numpy(), ref.numpy())
+
+        def r6(m):
+            return {k: round(float(v), 6) for k, v in m.items()}
+
+        return {"sample": f"{ref.shape[0]} impressions x {C} candidates of the timed batch (news ids); fp32 "
+                          "reference CPU path (oracle) vs the GPU news path; labels ~ Bernoulli(sigmoid(2 z(ref)))",
+                "reference_cpu": r6(mr), "gpu_fp32": r6(m32), "gpu_bf16": r6(m16),
+                "max_abs_metric_delta_fp32": float(max(abs(m32[k] - mr[k]) for k in mr)),
+                "max_abs_metric_delta_bf16": float(max(abs(m16[k] - mr[k]) for k in mr)),
+                "fp32_scores_within_parity_tol": ok, "fp32_worst_frac_of_tol": round(worst, 4)}
+    except Exception as e:  # a reporting leg: it never takes the bench line down
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def run_news(args, rank, world, dev):
     """BASELINE config 3 on the news-id input: every step recomputes the per-news
     precompute over the whole table (news_pre) and scores a batch of impressions (news_score)."""
@@ -397,6 +445,7 @@ def run_news(args, rank, world, dev):
            "tflops": round(pre_fl / (pre_ms / 1e3) / 1e12, 2),
            "frac_bf16_peak": round(pre_fl / (pre_ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
     cpu = cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
+    auc = auc_parity(nt, pool[0], table, W1, Q, W2, dev) if (world == 1 and not args.no_cpu) else None
     line = {
         "metric": "(user,candidate) scores/sec at history=50,K=32,d=768; AUC parity vs ref",
         "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
@@ -410,7 +459,7 @@ def run_news(args, rank, world, dev):
                    "impressions_per_gpu_per_step": B, "global_batch": B * world,
                    "parallelism": f"dp{world} (impression shards, no data-path collective)"},
         "roofline": roof, "precompute": pre, "fp32_parity_mode": f32, "dense_rows_kernel": dense,
-        "cpu_baseline": cpu,
+        "cpu_baseline": cpu, "auc_parity": auc,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

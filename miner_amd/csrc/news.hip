@@ -269,8 +269,8 @@ struct NsParams {
   float* scores;
   float* mui_out;
   int n_news, B, L, C, d, K, score_type;
-  int abl;      // ablation bits for diagnosis (MINER_NEWS_ABL): 1 no chunk compute, 2 no row DMAs,
-                // 4 no softmax, 8 no S7, 16 no aux DMAs, 32 no barrier
+  int abl;      // experiment bits (MINER_NEWS_ABL, A/B in one process): 1 = no priority for waves 4-7
+
 };
 
 #ifdef MINER_NEWS_DEBUG
@@ -389,12 +389,34 @@ __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpre
 #else
 #define NEWS_CP_STR ""
 #endif
-template <class T, int CW>
-__device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC, const char* bE, const char* bY,
-                                          unsigned mE) {
-  using Cf = NCfg<T, CW>;
+// one row DMA (saddr form) into M0 = m, M0 saved and restored around it
+__device__ __forceinline__ void dma_row(uint32_t off, const char* base, unsigned m) {
   unsigned t;
-  if constexpr (Cf::NI == 1) {
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" NEWS_CP_STR "\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(off), "s"(base), "s"(m) : "memory");
+}
+
+// SKIP (PD == 1 only, where the slot wait is vmcnt(0) and no count depends on how many DMAs a chunk
+// issued): a DMA instruction whose rows all lie past L (history) or past the pass's candidate count is
+// not issued (bit jj of `live`: history rows of E and proj; bit NI + jj: candidate rows). Those ring
+// rows keep the zeros written at kernel start (or a finite row of an earlier chunk): they meet only
+// A = 0 history slots and candidate rows whose scores are never stored. proj rows only for 'weighted'.
+template <class T, int CW, bool SKIP, bool WITH_PROJ>
+__device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC, const char* bE, const char* bY,
+                                          unsigned mE, unsigned live) {
+  using Cf = NCfg<T, CW>;
+  [[maybe_unused]] unsigned t;
+  if constexpr (SKIP) {
+#pragma unroll
+    for (int jj = 0; jj < Cf::NI; ++jj) {
+      if (live & (1u << jj)) {
+        dma_row(oH[jj], bE, mE + jj * kWaves * 1024);
+        if constexpr (WITH_PROJ) dma_row(oH[jj], bY, mE + Cf::PART + jj * kWaves * 1024);
+      }
+      if (live & (1u << (Cf::NI + jj))) dma_row(oC[jj], bE, mE + 2 * Cf::PART + jj * kWaves * 1024);
+    }
+  } else if constexpr (Cf::NI == 1) {
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3" NEWS_CP_STR "\n\t"
@@ -433,6 +455,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   static_assert(PD >= 1 && PD <= NS - 1, "prefetch depth");
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
   constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
+  constexpr bool SKIP = PD == 1;              // padding-row DMAs not issued (dma_chunk)
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int L = p.L, d = p.d;
@@ -571,12 +594,20 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   };
   // this lane's row offsets (bytes, + its swizzled 16-byte piece) for item (i, pass): the history
   // row (E and proj parts) and the candidate row of each of its NI DMA blocks
-  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC) {
+  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC, unsigned& lv) {
     const int lane = threadIdx.x & 63;
     const bool live = i < n_i;
     int off = 0, cnt = 1;
     if (live) cands(i, off, cnt);
     const int cntp = max(1, min(64, cnt - 64 * pass));
+    lv = 0;                            // live DMA instructions of this wave (dma_chunk, SKIP)
+#pragma unroll
+    for (int jj = 0; jj < NI; ++jj) {
+      const int row0 = (wave + 8 * jj) * Cf::RPI;   // first row of instruction jj
+      if (live && row0 < L) lv |= 1u << jj;
+      if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 1u << (NI + jj);
+    }
+    lv = __builtin_amdgcn_readfirstlane(lv);
     const int* hid = l1_his(smem, i & 3);
     const int* cid = l1_cand(smem, i & 3);
     const uint32_t rowBytes = (uint32_t)d * sizeof(T);
@@ -705,6 +736,12 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     }
   };
 
+  // ring rows no DMA writes (history slots >= L, candidates past the count) read as zeros; the
+  // prologue's first barrier (lgkmcnt(0)) orders these stores before every ring DMA
+  if constexpr (SKIP) {
+    for (int o = (int)threadIdx.x * 16; o < kRingB; o += kThreads * 16)
+      *reinterpret_cast<u32x4*>(smem + o) = u32x4{0u, 0u, 0u, 0u};
+  }
   // ---- prologue: aux for the first impressions, A of impression 0, then the first PD chunks ----
   for (int i = 0; i < 4; ++i) issue_L0(i);
   vm_wait_all();
@@ -723,10 +760,12 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     raw_barrier();
   }
   uint32_t cH[NI], cC[NI], nH[NI], nC[NI];   // row offsets of the current / next item
-  item_offsets(0, 0, cH, cC);
+  unsigned cLv = 0, nLv = 0;                 // and their live DMA instructions
+  item_offsets(0, 0, cH, cC, cLv);
 #pragma unroll
   for (int k = 0; k < PD; ++k)
-    dma_chunk<T, CW>(cH, cC, tabB + k * CW * sizeof(T), prjB + k * CW * sizeof(T), sbase + k * Cf::SLOT + wave * 1024);
+    dma_chunk<T, CW, SKIP, WEIGHTED>(cH, cC, tabB + k * CW * sizeof(T), prjB + k * CW * sizeof(T),
+                                     sbase + k * Cf::SLOT + wave * 1024, cLv);
 
   f32x16 acc[NT];                      // this wave's M / Lg partials, 32x32 candidate tiles
 #pragma unroll
@@ -790,12 +829,17 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     }
   };
 
+  // static priority for the X-path waves 4-7 (the GELU chain, the longer one of each SIMD's pair):
+  // MI355X_MICROARCH.md §Two waves per SIMD, item 4. Config 3: 4.37 -> 4.20 ms, bit-identical.
+  if (!(p.abl & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
+
   // one 64-column chunk: the row DMAs of chunk `ich` of the item whose offsets are (iH, iC), PD
   // chunks ahead, then the X / mui slab and the candidate product of this chunk.
   // `mode`: 1 X, 2 candidate product, 4 mui out
-  auto chunk = [&](int ci, int cc, int mode, int ncand, const uint32_t* iH, const uint32_t* iC, int ich) {
-    dma_chunk<T, CW>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
-                     sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024);
+  auto chunk = [&](int ci, int cc, int mode, int ncand, const uint32_t* iH, const uint32_t* iC, unsigned iLv,
+                   int ich) {
+    dma_chunk<T, CW, SKIP, WEIGHTED>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
+                                     sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024, iLv);
     if (mode & 1) {
       FRESH_LANE_IDS();
       const char* slot = smem + (t & (NS - 1)) * Cf::SLOT;
@@ -823,10 +867,10 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         for (int e = 0; e < 16; e += 4) *reinterpret_cast<float4*>(dst + e) = make_float4(ax[e], ax[e + 1], ax[e + 2], ax[e + 3]);
       }
       if (mode & 2) {
+        const char* cpart = slot + 2 * Cf::PART;
         if (WEIGHTED && P == 1) gelu_tile<T>(ax);
         Frag<T> xf;
         acc_to_frag<T>(xf, ax);
-        const char* cpart = slot + 2 * Cf::PART;
 #pragma unroll
         for (int tl = 0; tl < NT; ++tl) {
           if (tl == 0 || ncand > 32) {
@@ -891,13 +935,13 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       for (; cc < nchunk - PD; ++cc, ++t) {
         wait_slot();
         extras(cc);
-        chunk(ci, cc, mode, cntp, cH, cC, cc + PD);
+        chunk(ci, cc, mode, cntp, cH, cC, cLv, cc + PD);
       }
-      item_offsets(ni, np, nH, nC);
+      item_offsets(ni, np, nH, nC, nLv);
       for (; cc < nchunk; ++cc, ++t) {
         wait_slot();
         extras(cc);
-        chunk(ci, cc, mode, cntp, nH, nC, cc + PD - nchunk);
+        chunk(ci, cc, mode, cntp, nH, nC, nLv, cc + PD - nchunk);
       }
       // pass done: partials -> LDS blocks [c][k ^ swizzle] (block = 4P + 2 sl + tile for the two
       // slab halves that survive), S7 at the next item's first chunk
@@ -940,6 +984,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       pend_cnt = cntp;
 #pragma unroll
       for (int jj = 0; jj < NI; ++jj) { cH[jj] = nH[jj]; cC[jj] = nC[jj]; }
+      cLv = nLv;
     }
   }
   vm_wait_all();
