@@ -441,7 +441,7 @@ def run_news(args, rank, world, dev):
                     "candidates) + logit rows + ids + mask + scores; traffic = PMC HBM bytes per launch "
                     "(rows re-read by other impressions hit L2 / the Infinity Cache)"}
     pre_fl = news_precompute_flops(N_NEWS, D, DC, K)
-    pre = {"kernel": "news_pre<bf16>", "ms": round(pre_ms, 4), "flops": pre_fl,
+    pre = {"kernel": "news_pre2<bf16> (GEMM-shaped)", "ms": round(pre_ms, 4), "flops": pre_fl,
            "tflops": round(pre_fl / (pre_ms / 1e3) / 1e12, 2),
            "frac_bf16_peak": round(pre_fl / (pre_ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
     cpu = cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None

@@ -254,6 +254,155 @@ __global__ __launch_bounds__(kThreads) void news_pre(PreParams p) {
   vm_wait_all();
 }
 
+// GEMM-shaped precompute (bf16): one persistent workgroup per CU walks 256-row x 256-column output
+// tiles of [n_news, W1 (Dc, padded to 8 tiles) | W2 (d)], tile t -> (row tile, column tile) so that
+// the 4 column tiles of a row tile land on one XCD (blocks b, b+8, b+16, b+24) and re-read the rows
+// from its L2. Per 32-column slab of d (one "step") the 8 packed weight tiles of the column tile
+// (2 KiB each, fragment-major) and the 256 row pieces (64 B each, XOR-swizzled) are LDS-DMA'd into a
+// 4-slot ring, 3 steps ahead, across tile boundaries; every weight byte staged serves 256 rows (the
+// register-streamed news_pre re-reads all weights per 64 rows). Wave w owns rows [32w, 32w+32) and
+// all 8 column tiles, so for the W1 tile the logits tanh(P)·Qᵀ are summed over the Dc tiles in
+// registers (Q staged in LDS once); W2 tiles store proj straight from the accumulators.
+constexpr int kP2Rows = 256;
+constexpr int kP2RowB = 64;                                 // bytes of one staged row piece (32 bf16)
+constexpr int kP2Slot = kP2Rows * kP2RowB + 8 * 2048;       // rows | 8 weight tiles
+constexpr int kP2NS = 4;
+constexpr int kP2QOff = kP2NS * kP2Slot;                    // packed Q (32 x nct*32 bf16) after the ring
+__device__ __forceinline__ int p2_swz(int row) { return (row >> 2) & 3; }
+
+template <int NSL>
+__global__ __launch_bounds__(kThreads) void news_pre2(PreParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using T = __bf16;
+  const int d = p.d;
+  const int ns = NSL > 0 ? NSL : (d >> 5);
+  const int nct = n_ct(p.Dc);
+  const int ncol = 1 + (p.proj ? (d + 255) / 256 : 0);
+  const int nrt = (p.N + kP2Rows - 1) / kP2Rows;
+  const int ntile = ((nrt + 7) & ~7) * ncol;
+  const T* __restrict__ W1p = static_cast<const T*>(p.wp);
+  const T* __restrict__ Qp = W1p + w1p_el(d, p.Dc);
+  const T* __restrict__ W2p = Qp + qp_el(p.Dc);
+  const T* __restrict__ tab = static_cast<const T*>(p.table);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
+  const int G = gridDim.x;
+  const int my_tiles = ((int)blockIdx.x < ntile) ? (ntile - (int)blockIdx.x + G - 1) / G : 0;
+  const int nq = my_tiles * ns;
+  auto tile_pos = [&](int t, int& rt, int& ct) {
+    const int grp = t / (8 * ncol), i = t - grp * 8 * ncol;
+    rt = grp * 8 + (i & 7);
+    ct = i >> 3;
+  };
+  // step q of this workgroup -> its 4 DMAs per wave (2 weight-tile halves, 2 row instructions);
+  // out-of-range tiles and rows are clamped to valid memory, never consumed
+  auto issue = [&](int q) {
+    const int lane = threadIdx.x & 63;
+    int rt, ct;
+    tile_pos((int)blockIdx.x + (q / ns) * G, rt, ct);
+    const int sl = q % ns;
+    const unsigned slot = sbase + (q & (kP2NS - 1)) * kP2Slot;
+    const T* blk = W1p;
+    if (ct == 0) {
+      if (wave < nct) blk = W1p + ((size_t)wave * ns + sl) * 1024;
+    } else {
+      const int j2 = 8 * (ct - 1) + wave;
+      if (j2 < ns) blk = W2p + ((size_t)j2 * ns + sl) * 1024;
+    }
+    dma_b128_c(blk + lane * 8, slot + kP2Rows * kP2RowB + wave * 2048);
+    dma_b128_c(blk + 512 + lane * 8, slot + kP2Rows * kP2RowB + wave * 2048 + 1024);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 2 * wave + h;
+      const int row = 16 * j + (lane >> 2), pc = lane & 3;
+      const int n = min(rt * kP2Rows + row, p.N - 1);
+      dma_b128_c(tab + (size_t)n * d + 32 * sl + 8 * (pc ^ p2_swz(row)), slot + j * 1024);
+    }
+  };
+
+  // packed Q -> LDS (plain loads; the first barrier below publishes it)
+  {
+    const int nqe = 32 * nct * 32;                         // bf16 elements
+    const u32x4* src = reinterpret_cast<const u32x4*>(Qp);
+    u32x4* dst = reinterpret_cast<u32x4*>(smem + kP2QOff);
+    for (int i = threadIdx.x; i < nqe / 8; i += kThreads) dst[i] = src[i];
+  }
+  for (int q = 0; q < min(kP2NS - 1, nq); ++q) issue(q);
+
+  f32x16 acc[8];
+  for (int q = 0; q < nq; ++q) {
+    const int sl = q % ns;
+    if (sl == 0) {
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) acc[jt] = zero16();
+    }
+    const int younger = min(nq - 1 - q, kP2NS - 2);       // steps issued after q (4 DMAs each)
+    if (younger >= 2) vm_wait<8>();
+    else if (younger == 1) vm_wait<4>();
+    else vm_wait<0>();
+    raw_barrier();                                         // step q landed for all; slot of q-1 free
+    if (q + kP2NS - 1 < nq) issue(q + kP2NS - 1);
+    int rt, ct;
+    tile_pos((int)blockIdx.x + (q / ns) * G, rt, ct);
+    const int nvalid = ct == 0 ? nct : min(8, ns - 8 * (ct - 1));   // column tiles of this tile
+    {
+      FRESH_LANE_IDS();
+      const char* slot = smem + (q & (kP2NS - 1)) * kP2Slot;
+      const int row = 32 * wave + r;
+      Frag<T> ef;
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) ef.q[qq] = lds_u32x4(slot + row * kP2RowB + (((2 * h + qq) ^ p2_swz(row)) << 4));
+      const char* wst = slot + kP2Rows * kP2RowB;
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) {
+        if (jt < nvalid) {
+          Frag<T> wf;
+          wf.q[0] = lds_u32x4(wst + jt * 2048 + lane * 16);
+          wf.q[1] = lds_u32x4(wst + jt * 2048 + 1024 + lane * 16);
+          mma_slab(acc[jt], wf, ef);
+        }
+      }
+    }
+    if (sl == ns - 1) {                                    // tile done: epilogue
+      FRESH_LANE_IDS();
+      const int n = rt * kP2Rows + 32 * wave + r;
+      if (ct == 0) {
+        // Sᵀ [k, news] = Σ_tiles Q[:, tile] · tanh(Pᵀ)[tile, news]; Q rows in pi order (model.py:171-174)
+        f32x16 sacc = zero16();
+        const char* ql = smem + kP2QOff;
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) {
+          if (jt < nct) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[jt][e] = tanh_fast(acc[jt][e]);
+            Frag<T> pf, qf;
+            acc_to_frag<T>(pf, acc[jt]);
+            const char* qa = ql + ((size_t)pi_row(r) * (nct * 32) + 32 * jt + 16 * h) * 2;
+            qf.q[0] = lds_u32x4(qa);
+            qf.q[1] = lds_u32x4(qa + 16);
+            mma_slab(sacc, qf, pf);
+          }
+        }
+        if (n < p.N) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (16 * h + e < p.K) p.logits[(size_t)n * p.K + 16 * h + e] = sacc[e];
+        }
+      } else if (n < p.N) {
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) {
+          if (jt < nvalid) {
+            Frag<T> of;
+            acc_to_frag<T>(of, acc[jt]);
+            frag_store(static_cast<T*>(p.proj) + (size_t)n * d + 32 * (8 * (ct - 1) + jt) + 16 * h, of);
+          }
+        }
+      }
+    }
+  }
+  vm_wait_all();
+}
+
 // ================================================================================================
 // per-impression scoring
 // ================================================================================================
@@ -1034,8 +1183,22 @@ int launch_pre(void* stream, const PreParams& prm, int lds) {
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
+template <int NSL>
+int launch_pre2(void* stream, const PreParams& prm) {
+  auto kern = news_pre2<NSL>;
+  const int lds = kP2QOff + 32 * n_ct(prm.Dc) * 32 * 2;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(kern, dim3(num_cus()), dim3(kThreads), lds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
 template <class T>
 int run_pre(void* stream, const PreParams& prm, int lds) {
+  if constexpr (sizeof(T) == 2) {
+    if (!getenv("MINER_NEWS_PRE1")) return prm.d == 768 ? launch_pre2<24>(stream, prm) : launch_pre2<0>(stream, prm);
+  }
   switch (prm.d >> 5) {
     case 2: return launch_pre<T, 2>(stream, prm, lds);
     case 4: return launch_pre<T, 4>(stream, prm, lds);
