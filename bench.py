@@ -1,35 +1,41 @@
 """Benchmark: scored (user, candidate) pairs/s of the MINER scoring path on MI355X.
 
-    python bench.py [--gpus N --steps K --warmup W]            # N=1 default
+    python bench.py [--gpus N --steps K --warmup W]          # N=1 default; N>1 spawns N ranks itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json metric, config 3 "MIND-large shape"): history L=50, K=32 interests,
-d=768, Dc=200, C=40 candidates per impression, bf16 operands / fp32 accumulation. Impressions
-are given as news ids over a 104,000 x 768 news table (the reference's eval input: reader.py
-feeds news ids, the news encoder's output is a per-news table), ids and table resident in HBM.
+Headline (BASELINE.json metric, config 3 "MIND-large shape": history L=50, K=32 interests, d=768,
+Dc=200, C=40 candidates per impression), at the REFERENCE'S precision: fp32 operands and fp32
+arithmetic (the reference evaluates in fp32, src/trainer.py:278-281; scores match its CPU path to
+1e-5). Impressions are news ids over a 104,000 x 768 news table (the reference's eval input:
+reader.py feeds news ids, the news encoder's output is a per-news table), resident in HBM.
+
 One step = the per-news precompute over the WHOLE table (news_pre: tanh(E·W1ᵀ)·Qᵀ and E·W2ᵀ,
 SURVEY.md §8 f2) + one launch of the scoring kernel (news_score) over ``--batch`` impressions per
-GPU; impressions are sharded across ranks with no collective on the data path (weak scaling);
-``value`` = pairs scored by all ranks / max-over-ranks time.
+GPU (default 3,000,000 = the whole MIND-large-shaped eval set per GPU); impressions are sharded
+across ranks with no collective on the data path (weak scaling); ``value`` = pairs scored by all
+ranks / max-over-ranks time.
 
-Also reported (same JSON line): the HBM roofline of the scoring kernel (algorithmic bytes per
-launch over its HIP-event launch time, on the stream it runs on), the precompute's time, the fp32
-parity mode, the fused dense-row kernel (``--workload config3-dense``: weights per impression, rows
-given as [B, L, d] tensors) for comparison, and the CPU baseline (the oracle — a restatement of
-the reference's torch CPU path — timed on this host's cores over a bounded sample) at N=1.
+Also on the line: ``roofline`` of the scoring kernel on SURVEY §8(d)'s algorithmic bytes
+((L+C)·d·4 + L + 4C per impression) over its HIP-event launch time, with the MFMA fraction of its
+contraction FLOPs beside it and the bytes it really gathers (``gathered_bytes``); the bf16
+throughput mode of the same path (``bf16_mode``, with its AUC delta); config 2 (d=256, 50k
+impressions); the metric step (per-impression metrics + exact global AUC on the device); the fused
+dense-row kernel; the AUC parity of the GPU path against the reference CPU path on a sample; and
+the CPU baseline (the oracle — the reference's torch CPU path restated — on this host's cores) at
+N=1.
 
-``--workload corpus`` measures BASELINE config 5 (every user against a 200k-news table, history 200,
-K=64, fp16, fused click score + top-k); ``--workload fastformer`` measures
-BASELINE config 4 instead (the FastFormer user encoder,
-SURVEY.md §8 f3): 50,000 impressions per GPU per step, history 50, 40 candidates, hidden 256,
-bf16, same JSON contract.
+``--workload fastformer`` measures BASELINE config 4 (FastFormer user encoder), ``--workload corpus``
+config 5 (full-corpus ranking), ``--workload config3-dense`` the fused kernel on [B, L, d] rows.
+``--dry-run`` exercises the launcher and the timing protocol on the CPU (gloo), no kernel.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,29 +47,121 @@ import torch.distributed as dist  # noqa: E402
 
 L, K, D, DC, C = 50, 32, 768, 200, 40
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-PEAK_F32_TFLOPS = 157.3        # fp32 MFMA / vector
+PEAK_F32_TFLOPS = 157.3        # fp32 MFMA = fp32 vector (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0          # HBM3E spec
+METRIC = "(user,candidate) scores/sec at history=50,K=32,d=768; AUC parity vs ref"
 
 
+# ---------------------------------------------------------------------------------------------
+# algorithmic work
+# ---------------------------------------------------------------------------------------------
 def flops_per_impression(L, K, d, Dc, C):
-    """Algorithmic FLOPs: 2LdDc + 2LDcK + 2KLd + 2Kd² + 4CdK + 2CK."""
+    """Algorithmic FLOPs of the whole path: 2LdDc + 2LDcK + 2KLd + 2Kd² + 4CdK + 2CK."""
     return 2 * L * d * Dc + 2 * L * Dc * K + 2 * K * L * d + 2 * K * d * d + 4 * C * d * K + 2 * C * K
 
 
 def bytes_per_impression(L, d, C, elem):
-    """Algorithmic HBM bytes: (L + C)·d·s + L (mask) + 4C (fp32 scores); weights excluded."""
+    """SURVEY §8(d) algorithmic HBM bytes: (L + C)·d·s + L (mask) + 4C (fp32 scores); weights excluded."""
     return (L + C) * d * elem + L + 4 * C
 
 
-def cpu_baseline(seconds: float = 15.0):
-    """Oracle (torch fp32 CPU restatement of model.py:159-216,127) on host cores."""
+def news_gathered_bytes(L, d, C, K, elem):
+    """Bytes the news-path scoring kernel actually moves per impression: history rows of the table
+    AND of its projection (the E·W2ᵀ reformulation's second gather), candidate rows, the history
+    logit rows (fp32), ids, mask, fp32 scores. Not the roofline's numerator (that is §8(d))."""
+    return 2 * L * d * elem + C * d * elem + L * K * 4 + 4 * L + L + 4 * C + 4 * C
+
+
+def news_kernel_flops(L, K, d, C):
+    """Contraction FLOPs of the news-path scoring kernel per impression (unpadded): mui = A·E[his]
+    and X = A·proj[his] (2·2KLd), M = Cand·muiᵀ and Lg = Cand·Xᵀ (2·2CdK)."""
+    return 4 * K * L * d + 4 * C * d * K
+
+
+def news_precompute_flops(n_news, d, Dc, K):
+    """tanh(E·W1ᵀ)·Qᵀ and E·W2ᵀ over the table (model.py:171-174, :212)."""
+    return n_news * (2 * d * Dc + 2 * Dc * K + 2 * d * d)
+
+
+# ---------------------------------------------------------------------------------------------
+# timing protocol: W untimed steps, barrier + sync, K timed steps, barrier + sync, max over ranks
+# ---------------------------------------------------------------------------------------------
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def timed_steps(step, steps, warmup, world, dev):
+    """Runs step(i, timed) W times untimed then K times timed; returns max-over-ranks seconds."""
+    for i in range(warmup):
+        step(i, False)
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i, True)
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    _sync(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+class EventTimer:
+    """HIP events recorded on the stream the kernels run on (torch's current stream, where every
+    miner_amd op enqueues): per-step segment times in ms."""
+
+    def __init__(self, dev, n_seg):
+        self.stream = torch.cuda.current_stream(dev)
+        self.n = n_seg
+        self.ev = []
+
+    def step(self):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(self.n + 1)]
+        self.ev.append(e)
+        return e
+
+    def mean_ms(self, seg):
+        return sum(e[seg].elapsed_time(e[seg + 1]) for e in self.ev) / max(len(self.ev), 1)
+
+
+def host_info():
+    """Threads used by the CPU baseline, the host's CPUs and the CPU model (lscpu)."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return {"threads_used": torch.get_num_threads(), "host_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "cpu_model": model}
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU baselines (the oracle = the reference's torch CPU path restated; oracle/ is the checker)
+# ---------------------------------------------------------------------------------------------
+def cpu_baseline(seconds: float = 15.0, d: int = D):
+    """Oracle (torch fp32 CPU restatement of model.py:159-216,127) on host cores, config-3 shape."""
     from miner_amd import synthetic
     from oracle import miner_oracle as orc
-    threads = torch.get_num_threads()
-    imp = synthetic.impressions(36, 0, 512, L=L, d=D, C=C, device="cpu")
-    W1, Q, W2 = synthetic.init_weights(36, D, DC, K)
+    hi = host_info()
+    imp = synthetic.impressions(36, 0, 512, L=L, d=d, C=C, device="cpu")
+    W1, Q, W2 = synthetic.init_weights(36, d, DC, K)
     bs = 64
-    # batched layout: 64 impressions x 40 candidates per call
     with torch.no_grad():
         orc.score_torch(imp.history[:bs], imp.his_mask[:bs], imp.candidates[:bs], W1, Q, W2)  # warmup
         pairs, t0, i = 0, time.perf_counter(), 0
@@ -88,234 +186,160 @@ def cpu_baseline(seconds: float = 15.0):
             if el2 > seconds / 3 and n_imp >= 2:
                 break
         per_cand = n_imp * C / el2
-    return {"value": round(batched, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{pairs // C} impressions x {C} candidates (L={L},K={K},d={D},Dc={DC}), fp32, "
+    return {"value": round(batched, 1), "unit": "pairs/s", "cores": hi["threads_used"], "kind": "port",
+            "sample": f"{pairs // C} impressions x {C} candidates (L={L},K={K},d={d},Dc={DC}), fp32, "
                       f"batched 64 impressions/call, {el:.1f}s",
+            "host_cpus": hi["host_cpus"], "affinity_cpus": hi["affinity_cpus"], "cpu_model": hi["cpu_model"],
             "per_candidate_value": round(per_cand, 1),
             "per_candidate_sample": f"{n_imp} impressions, one candidate per sample, batch 32 "
                                     f"(reader.py:376-379 layout), {el2:.1f}s"}
 
 
-FF_L, FF_C, FF_H, FF_B = 50, 40, 256, 50000
-
-
-def ff_flops_per_impression(L=FF_L, C=FF_C, H=FF_H):
-    """Algorithmic FLOPs of the FastFormer user encoder + click predictor (model.py:345-545, :322):
-    per layer 6 H x H linears + 2 H -> 16 head projections + the 2 pooled attentions, then the
-    pooler (att_fc1, att_fc2, weighted sum) and C dot products; the MFMA pad of L to 64 excluded."""
-    layer = 6 * 2 * L * H * H + 2 * 2 * L * H * 16 + 2 * 2 * L * H
-    return 2 * layer + 2 * L * H * H + 2 * L * H + 2 * L * H + 2 * C * H
-
-
-def ff_bytes_per_impression(L=FF_L, C=FF_C, H=FF_H, elem=2):
-    """Algorithmic HBM bytes: history + candidate rows, mask, fp32 scores (parameters excluded)."""
-    return (L + C) * H * elem + L + 4 * C
-
-
-def ff_cpu_baseline(seconds: float = 15.0):
-    """FastFormer oracle (torch fp32 CPU restatement of model.py:345-545, :322) on host cores."""
-    from miner_amd import fastformer as ff
-    from miner_amd import synthetic
-    from oracle import fastformer_oracle as ffo
-    threads = torch.get_num_threads()
-    blob = synthetic.fastformer_params(0)
-    params = {n: t.reshape(shp) for (n, shp), t in
-              zip(ff.PARAMS, torch.split(blob, [int(torch.Size(shp).numel()) for _, shp in ff.PARAMS]))}
-    g = torch.Generator().manual_seed(1)
-    bs = 64
-    E = torch.randn(bs, FF_L, FF_H, generator=g) * 0.0625
-    M = torch.rand(bs, FF_L, generator=g) > 0.3
-    Cd = torch.randn(bs, FF_C, FF_H, generator=g) * 0.0625
-    with torch.no_grad():
-        ffo.scores(params, E, M, Cd)
-        pairs, t0, i = 0, time.perf_counter(), 0
-        while True:
-            ffo.scores(params, E, M, Cd)
-            pairs += bs * FF_C
-            i += 1
-            el = time.perf_counter() - t0
-            if el > seconds and i >= 2:
-                break
-    return {"value": round(pairs / el, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{pairs // FF_C} impressions x {FF_C} candidates (L={FF_L}, hidden {FF_H}), fp32, "
-                      f"batched {bs} impressions/call, {el:.1f}s"}
-
-
-def run_fastformer(args, rank, world, dev):
-    """BASELINE config 4: the FastFormer kernel over FF_B resident impressions per GPU per step."""
-    from miner_amd import fastformer as ff
-    from miner_amd import synthetic
-    B = args.batch if args.batch_set else FF_B
-    bf = torch.bfloat16
-    pool = []
-    for p in range(args.pool):
-        start = (rank * args.pool + p) * B
-        g = torch.Generator().manual_seed(1000 + start)
-        lens = torch.randint(0, FF_L + 1, (B,), generator=g)
-        mask = (torch.arange(FF_L)[None, :] >= (FF_L - lens)[:, None]).to(dev)
-        hist = (torch.randn(B, FF_L, FF_H, generator=g) * 0.0625).to(dev, bf)
-        cand = (torch.randn(B, FF_C, FF_H, generator=g) * 0.0625).to(dev, bf)
-        pool.append((hist, mask, cand))
-    blob = synthetic.fastformer_params(0).to(dev)
-    pk16 = ff.pack(blob, bf)
-    pk32 = ff.pack(blob, torch.float32)
-    torch.cuda.synchronize()
-
-    def step(i):
-        hist, mask, cand = pool[i % len(pool)]
-        return ff.score(hist, mask, cand, pk16)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+def metric_step_cpu_baseline(n_imp: int = 2000):
+    """The reference's metric step (evaluation.py:36-84: sklearn per impression + np.argsort per
+    impression, restated in oracle/metrics_oracle.py) on the host, seconds per impression."""
+    import numpy as np
+    from oracle import metrics_oracle as mo
+    rng = np.random.default_rng(0)
+    targets, probs = [], []
+    for _ in range(n_imp):
+        y = (rng.random(C) < 0.2).astype(np.int64)
+        y[0], y[1] = 1, 0
+        targets.append(list(y))
+        probs.append(list(rng.random(C)))
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        out = step(i)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    assert torch.isfinite(out).all()
-    f32 = None
-    if args.fp32_steps > 0:
-        hist, mask, cand = pool[0]
-        n32 = min(B, 5000)
-        h32, c32, m32 = hist[:n32].float(), cand[:n32].float(), mask[:n32]
-        ff.score(h32, m32, c32, pk32)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(args.fp32_steps):
-            ff.score(h32, m32, c32, pk32)
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms32 = a.elapsed_time(b) / args.fp32_steps
-        f32 = {"value": round(n32 * FF_C / (ms32 / 1e3), 1), "unit": "pairs/s", "ms_per_step": round(ms32, 3),
-               "impressions": n32,
-               "tflops": round(ff_flops_per_impression() * n32 / (ms32 / 1e3) / 1e12, 2)}
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
-    value = B * FF_C * args.steps * world / elapsed
-    fl = ff_flops_per_impression() * B
-    by = ff_bytes_per_impression() * B
-    tflops = fl / (kern_ms / 1e3) / 1e12
-    gbs = by / (kern_ms / 1e3) / 1e9
-    roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": "ff_fused<bf16>",
-            "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4)}
-    roof_hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_launch": by}
-    cpu = ff_cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
-    line = {
-        "metric": "(user,candidate) scores/sec, FastFormer user encoder (config 4)",
-        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-        "data": "synthetic (seeded config-4-shaped impressions, random-init weights)",
-        "config": {"workload": "config 4 FastFormer user encoder", "history": FF_L, "hidden": FF_H,
-                   "heads": 16, "layers": 2, "candidates": FF_C, "impressions_per_gpu_per_step": B,
-                   "global_batch": B * world,
-                   "parallelism": f"dp{world} (impression shards, no data-path collective)"},
-        "roofline": roof, "roofline_hbm": roof_hbm, "fp32_parity_mode": f32, "cpu_baseline": cpu,
-    }
-    print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    mo.compute_scores(targets, probs, ["auc", "group_auc", "mrr", "ndcg@5", "ndcg@10", "hit@5", "hit@10"])
+    el = time.perf_counter() - t0
+    return {"ms_per_impression": round(el / n_imp * 1e3, 4), "sample": f"{n_imp} impressions x {C} candidates, "
+            "7 metrics (auc, group_auc, mrr, ndcg@5/10, hit@5/10), one thread"}
 
 
+# ---------------------------------------------------------------------------------------------
+# config 3 headline: the news-id path
+# ---------------------------------------------------------------------------------------------
 N_NEWS = 104_000     # MIND-large-shaped news table (SURVEY.md §8 f2: ~104k news x 768)
-NEWS_B = 131_072     # impressions per GPU per step (news-id input: 47 MB of ids per batch)
+NEWS_B = 3_000_000   # impressions per GPU per step: the whole MIND-large-shaped eval set (config 3)
+C2_B, C2_D, C2_NEWS = 50_000, 256, 65_238   # config 2 (MIND-small shape: ~65k news)
 
 
-def news_bytes_per_impression(L, d, C, K, elem):
-    """Algorithmic bytes of the news-path scoring kernel per impression: the gathered history rows
-    of the table and of its projection, the candidate rows, the history logit rows (fp32), the ids,
-    the mask and the fp32 scores (the per-news precompute is a separate launch)."""
-    return 2 * L * d * elem + C * d * elem + L * K * 4 + 4 * L + L + 4 * C + 4 * C
+def news_batch(seed, B, n_news, dev, chunk=1 << 20):
+    """Impressions as news ids (the reference's eval input, reader.py:351-379): history length
+    ~ U{0..L}, left-padded with the pad news (row 0, reader.py:101-110, :369); candidates uniform."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    hid = torch.empty((B, L), dtype=torch.int32, device=dev)
+    mask = torch.empty((B, L), dtype=torch.bool, device=dev)
+    cid = torch.empty((B, C), dtype=torch.int32, device=dev)
+    pos = torch.arange(L, device=dev)
+    for s in range(0, B, chunk):
+        e = min(s + chunk, B)
+        lens = torch.randint(0, L + 1, (e - s,), generator=g, device=dev)
+        m = pos[None, :] >= (L - lens)[:, None]
+        h = torch.randint(1, n_news, (e - s, L), generator=g, device=dev, dtype=torch.int32)
+        hid[s:e] = torch.where(m, h, torch.zeros_like(h))
+        mask[s:e] = m
+        cid[s:e] = torch.randint(1, n_news, (e - s, C), generator=g, device=dev, dtype=torch.int32)
+    return hid, mask, cid
 
 
-def news_precompute_flops(n_news, d, Dc, K):
-    """tanh(E·W1ᵀ)·Qᵀ and E·W2ᵀ over the table (model.py:171-174, :212)."""
-    return n_news * (2 * d * Dc + 2 * Dc * K + 2 * d * d)
-
-
-def load_news_traffic(path, B):
+def load_pmc(path, workload, B):
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("workload") == f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_bf16" and t.get("batch") == B:
+        if t.get("workload") == workload and t.get("batch") == B:
             return t
     except (OSError, ValueError):
         pass
     return None
 
 
-def news_batch(seed, B, dev):
-    """Impressions as news ids (the reference's eval input, reader.py:351-379): history length
-    ~ U{0..L}, left-padded with the pad news (row 0, reader.py:101-110, :369); candidates uniform."""
-    g = torch.Generator(device=dev).manual_seed(seed)
-    lens = torch.randint(0, L + 1, (B,), generator=g, device=dev)
-    mask = torch.arange(L, device=dev)[None, :] >= (L - lens)[:, None]
-    hid = torch.randint(1, N_NEWS, (B, L), generator=g, device=dev, dtype=torch.int32)
-    hid[~mask] = 0
-    cid = torch.randint(1, N_NEWS, (B, C), generator=g, device=dev, dtype=torch.int32)
-    return hid, mask, cid
+def measure_news(table, W1, Q, W2, pool, steps, warmup, world, dev):
+    """One dtype of the news path: per step precompute + score over pool[i % len(pool)].
+    Returns (elapsed s, precompute ms, scoring ms, last scores, NewsTable)."""
+    from miner_amd import news, ops
+    pw = ops.pack_weights(W1, Q, W2, dtype=table.dtype)      # once per model, outside the timed region
+    nt = news.precompute(table, pw)
+    tm = EventTimer(dev, 2)
+    out = [None]
+
+    def step(i, timed):
+        nonlocal nt
+        hid, mask, cid = pool[i % len(pool)]
+        e = tm.step() if timed else None
+        if e:
+            e[0].record(tm.stream)
+        nt = news.precompute(table, pw, out=nt)
+        if e:
+            e[1].record(tm.stream)
+        out[0] = news.score(nt, hid, mask, cid, validate=False)
+        if e:
+            e[2].record(tm.stream)
+
+    elapsed = timed_steps(step, steps, warmup, world, dev)
+    return elapsed, tm.mean_ms(0), tm.mean_ms(1), out[0], nt
 
 
-def dense_kernel_line(dev, B=32768, steps=5):
-    """The fused dense-row kernel (weights per impression, miner_score) on the same shape, for
-    comparison: pairs/s and its MFMA fraction."""
-    from miner_amd import ops, synthetic
-    imp = synthetic.impressions(36, 0, B, L=L, d=D, C=C, device=dev, dtype=torch.bfloat16)
-    W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
-    pw = ops.pack_weights(W1, Q, W2, dtype=torch.bfloat16)
-    ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+def roofline_news(B, kern_ms, elem, d=D, pmc=None, kernel=""):
+    by = bytes_per_impression(L, d, C, elem) * B
+    gbs = by / (kern_ms / 1e3) / 1e9
+    fl = news_kernel_flops(L, K, d, C) * B
+    tf = fl / (kern_ms / 1e3) / 1e12
+    peak_tf = PEAK_F32_TFLOPS if elem == 4 else PEAK_BF16_TFLOPS
+    gathered = news_gathered_bytes(L, d, C, K, elem)
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "kernel": kernel, "kernel_ms": round(kern_ms, 4), "impressions_per_launch": B,
+            "algorithmic_bytes_per_impression": bytes_per_impression(L, d, C, elem),
+            "algorithmic_bytes_per_launch": by,
+            "mfma": {"flops_per_impression": news_kernel_flops(L, K, d, C), "achieved_tflops": round(tf, 2),
+                     "peak_tflops": peak_tf, "frac": round(tf / peak_tf, 4),
+                     "busy_frac_pmc": pmc.get("mfma_busy_frac") if pmc else None},
+            "gathered_bytes": {"per_impression": gathered, "per_launch": gathered * B,
+                               "achieved_gbs": round(gathered * B / (kern_ms / 1e3) / 1e9, 1)},
+            "note": "achieved/frac: SURVEY §8(d) bytes (L+C)·d·s + L + 4C per impression (weights and the "
+                    "per-news precompute excluded) over the HIP-event launch time; gathered_bytes: what the "
+                    "kernel moves (history rows of the table and of its projection, candidates, logit rows, ids, "
+                    "scores; re-reads served by L2 / the Infinity Cache); traffic: PMC HBM bytes per launch "
+                    "(2·FETCH_SIZE + WRITE_SIZE, gfx950 correction); mfma: the kernel's contraction FLOPs "
+                    "(2·2KLd + 2·2CdK, unpadded) vs the dense peak of the dtype"}
+
+
+def device_metrics(scores, dev):
+    """The reference's metric step (evaluation.py:36-84) over every impression of the batch, on the
+    device (per-impression kernel + exact global AUC); labels Bernoulli(sigmoid(2 z(scores))) with
+    >= 1 click and >= 1 non-click per impression (reader.py:374). Returns (labels, offsets, metrics,
+    ms)."""
+    from miner_amd import metrics
+    s = scores.float()
+    g = torch.Generator(device=dev).manual_seed(7)
+    z = (s - s.mean()) / s.std()
+    lab = (torch.rand(s.shape, generator=g, device=dev) < torch.sigmoid(2.0 * z)).to(torch.uint8)
+    rows = torch.arange(s.shape[0], device=dev)
+    lab[rows, s.argmax(1)] = 1
+    lab[rows, s.argmin(1)] = 0
+    offs = torch.arange(0, (s.shape[0] + 1) * C, C, dtype=torch.int32, device=dev)
+    names = ["auc", "group_auc", "mrr", "ndcg@5", "ndcg@10", "hit@5", "hit@10"]
     torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(steps):
-        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
-    b.record()
+    t0 = time.perf_counter()
+    m = metrics.compute_metrics(torch.sigmoid(s).reshape(-1), lab.reshape(-1), offs, names)
     torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / steps
-    tf = flops_per_impression(L, K, D, DC, C) * B / (ms / 1e3) / 1e12
-    del imp
-    return {"kernel": "miner_fused<bf16,full>", "value": round(B * C / (ms / 1e3), 1), "unit": "pairs/s",
-            "ms_per_launch": round(ms, 4), "impressions": B, "tflops": round(tf, 2),
-            "frac_bf16_peak": round(tf / PEAK_BF16_TFLOPS, 4)}
+    return lab, offs, m, (time.perf_counter() - t0) * 1e3
 
 
-def auc_parity(nt16, batch, table, W1, Q, W2, dev, n_imp=2048):
+def auc_parity(nt16, nt32, batch, table32, W1, Q, W2, dev, n_imp=2048):
     """The metric's "AUC parity vs ref", on a bounded sample of the timed batch (part of the CPU
     baseline leg): scores of the reference CPU path (the oracle: model.py:113-216 as the same torch
-    fp32 ops on the host) vs the GPU news path in its fp32 parity mode and in bf16, then the
-    reference's metrics (evaluation.py:36-84, via the GPU metrics kernel) over one set of labels:
+    fp32 ops on the host) vs the GPU news path in fp32 (the headline mode) and in bf16, then the
+    reference's metrics (evaluation.py:36-84, via the GPU metrics kernels) over one set of labels:
     Bernoulli(sigmoid(2·z)) of the reference's z-scored scores, with >= 1 click and >= 1 non-click per
     impression (reader.py:374)."""
     try:
-        from miner_amd import metrics, news, ops
+        from miner_amd import metrics, news
         from oracle import miner_oracle as orc
         hid, mask, cid = [x[:n_imp] for x in batch]
-        t32 = table.float()
-        nt32 = news.precompute(t32, ops.pack_weights(W1, Q, W2, dtype=torch.float32))
         s32 = news.score(nt32, hid, mask, cid, validate=False)
         s16 = news.score(nt16, hid, mask, cid, validate=False)
-        T = t32.cpu()
+        T = table32.cpu()
         h, c = hid.cpu().long(), cid.cpu().long()
         with torch.no_grad():
             _, ref = orc.score_torch(T[h], mask.cpu(), T[c], W1.cpu(), Q.cpu(), W2.cpu())
@@ -348,124 +372,253 @@ def auc_parity(nt16, batch, table, W1, Q, W2, dev, n_imp=2048):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def config2_line(args, rank, world, dev):
+    """BASELINE config 2 (MIND-small shape: 50k impressions, L=50, K=32, d=256, bf16) on the news
+    path, plus its fp32 parity mode; roofline on §8(d) bytes."""
+    from miner_amd import synthetic
+    out = {"workload": "config 2 MIND-small shape, news-id input", "impressions_per_gpu_per_step": C2_B,
+           "d": C2_D, "news_table": C2_NEWS}
+    g = torch.Generator(device=dev).manual_seed(2)
+    t32 = torch.randn((C2_NEWS, C2_D), generator=g, device=dev) / C2_D ** 0.5
+    W1, Q, W2 = synthetic.init_weights(2, C2_D, DC, K, device=dev)
+    pool = [news_batch(1000 + rank, C2_B, C2_NEWS, dev)]
+    for name, tab in (("bf16", t32.to(torch.bfloat16)), ("fp32", t32)):
+        el, pre_ms, kern_ms, _, _ = measure_news(tab, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+        elem = 2 if name == "bf16" else 4
+        out[name] = {"value": round(C2_B * C * args.steps * world / el, 1), "unit": "pairs/s",
+                     "ms_per_step": round(el / args.steps * 1e3, 4), "precompute_ms": round(pre_ms, 4),
+                     "roofline": roofline_news(C2_B, kern_ms, elem, d=C2_D, kernel=f"news_score<{name},weighted>")}
+    out["value"] = out["bf16"]["value"]
+    out["dtype"] = "bf16 (config 2's dtype); fp32 parity mode beside it"
+    return out
+
+
 def run_news(args, rank, world, dev):
-    """BASELINE config 3 on the news-id input: every step recomputes the per-news
-    precompute over the whole table (news_pre) and scores a batch of impressions (news_score)."""
-    from miner_amd import news, ops, synthetic
-    B = args.batch if args.batch_set else NEWS_B
-    bf = torch.bfloat16
+    """BASELINE config 3 on the news-id input, fp32 headline: every step recomputes
+    the per-news precompute over the whole table (news_pre) and scores a batch of impressions
+    (news_score)."""
+    from miner_amd import synthetic
+    B = args.batch or NEWS_B
     g = torch.Generator(device=dev).manual_seed(36)
-    table = (torch.randn((N_NEWS, D), generator=g, device=dev) / D ** 0.5).to(bf)
+    table32 = torch.randn((N_NEWS, D), generator=g, device=dev) / D ** 0.5
     W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
-    pw16 = ops.pack_weights(W1, Q, W2, dtype=bf)        # once per model, outside the timed region
-    pool = [news_batch(36 + (rank * args.pool + p) * B, B, dev) for p in range(args.pool)]
-    nt = news.precompute(table, pw16)
+    pool = [news_batch(36 + (rank * args.pool + p), B, N_NEWS, dev) for p in range(args.pool)]
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
 
-    def step(i, ev=None):
-        nonlocal nt
-        hid, mask, cid = pool[i % len(pool)]
-        if ev is not None:
-            ev[0].record(stream)
-        nt = news.precompute(table, pw16, out=nt)
-        if ev is not None:
-            ev[1].record(stream)
-        out = news.score(nt, hid, mask, cid, validate=False)
-        if ev is not None:
-            ev[2].record(stream)
-        return out
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        out = step(i, ev[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    pre_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    kern_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    assert torch.isfinite(out).all()
-
-    # fp32 parity mode of the same path (fewer steps; 32k impressions)
-    f32 = None
-    if args.fp32_steps > 0:
-        n32 = min(B, 32768)
-        hid, mask, cid = [x[:n32] for x in pool[0]]
-        t32 = table.float()
-        pw32 = ops.pack_weights(W1, Q, W2, dtype=torch.float32)
-        nt32 = news.precompute(t32, pw32)
-        news.score(nt32, hid, mask, cid, validate=False)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(args.fp32_steps):
-            nt32 = news.precompute(t32, pw32, out=nt32)
-            news.score(nt32, hid, mask, cid, validate=False)
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms32 = a.elapsed_time(b) / args.fp32_steps
-        f32 = {"value": round(n32 * C / (ms32 / 1e3), 1), "unit": "pairs/s", "ms_per_step": round(ms32, 3),
-               "impressions": n32, "note": "news path, fp32 operands and arithmetic (the parity mode)"}
-        del t32, nt32
-    dense = None
-    if world == 1 and not args.no_dense:
-        dense = dense_kernel_line(dev)
+    # headline: fp32 (the reference's precision)
+    el32, pre32, kern32, s32, nt32 = measure_news(table32, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+    assert torch.isfinite(s32).all()
+    # bf16 throughput mode, same batch and protocol
+    table16 = table32.to(torch.bfloat16)
+    el16, pre16, kern16, s16, nt16 = measure_news(table16, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+    assert torch.isfinite(s16).all()
+    c2 = config2_line(args, rank, world, dev) if not args.no_config2 else None
+    dense = dense_kernel_line(dev) if (world == 1 and not args.no_dense) else None
 
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
         return
-    value = B * C * args.steps * world / elapsed
-    by = news_bytes_per_impression(L, D, C, K, 2) * B
-    gbs = by / (kern_ms / 1e3) / 1e9
-    traffic = load_news_traffic(args.news_traffic, B)
-    roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(gbs / PEAK_HBM_GBS, 4),
-            "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-            "kernel": "news_score<bf16,weighted>", "algorithmic_bytes_per_launch": by,
-            "kernel_ms": round(kern_ms, 4),
-            "note": "algorithmic bytes = gathered rows (history of the table and of its projection, "
-                    "candidates) + logit rows + ids + mask + scores; traffic = PMC HBM bytes per launch "
-                    "(rows re-read by other impressions hit L2 / the Infinity Cache)"}
+    value = B * C * args.steps * world / el32
+    pmc32 = load_pmc(args.news_traffic32, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_fp32", B)
+    pmc16 = load_pmc(args.news_traffic, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_bf16", B)
+    roof = roofline_news(B, kern32, 4, pmc=pmc32, kernel="news_score<fp32,weighted>")
     pre_fl = news_precompute_flops(N_NEWS, D, DC, K)
-    pre = {"kernel": "news_pre2<bf16> (GEMM-shaped)", "ms": round(pre_ms, 4), "flops": pre_fl,
-           "tflops": round(pre_fl / (pre_ms / 1e3) / 1e12, 2),
-           "frac_bf16_peak": round(pre_fl / (pre_ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+    # metric step on the device over the whole fp32 batch, and the bf16 AUC delta at full size
+    metric_step = None
+    if not args.no_metrics:
+        lab, offs, m32, ms = device_metrics(s32, dev)
+        from miner_amd import metrics
+        m16 = metrics.compute_metrics(torch.sigmoid(s16.float()).reshape(-1), lab.reshape(-1), offs, list(m32))
+        metric_step = {"ms": round(ms, 2), "pairs": B * C, "impressions": B,
+                       "what": "per-impression group_auc/mrr/ndcg@5,10/hit@5,10 kernel + exact global AUC "
+                               "(device radix sort + rank sum) over the whole fp32 batch",
+                       "fp32": {k: round(float(v), 6) for k, v in m32.items()},
+                       "bf16_delta": {k: float(m16[k] - m32[k]) for k in m32},
+                       "cpu_reference": metric_step_cpu_baseline() if (world == 1 and not args.no_cpu) else None}
+    bf16_mode = {"value": round(B * C * args.steps * world / el16, 1), "unit": "pairs/s",
+                 "ms_per_step": round(el16 / args.steps * 1e3, 4), "precompute_ms": round(pre16, 4),
+                 "roofline": roofline_news(B, kern16, 2, pmc=pmc16, kernel="news_score<bf16,weighted>"),
+                 "auc_delta_vs_fp32": metric_step["bf16_delta"]["auc"] if metric_step else None,
+                 "note": "bf16 operands, fp32 accumulation: no reference counterpart (the reference evaluates "
+                         "in fp32); its metric deltas vs the fp32 headline are in metric_step.bf16_delta"}
     cpu = cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
-    auc = auc_parity(nt, pool[0], table, W1, Q, W2, dev) if (world == 1 and not args.no_cpu) else None
+    auc = auc_parity(nt16, nt32, pool[0], table32, W1, Q, W2, dev) if (world == 1 and not args.no_cpu) else None
     line = {
-        "metric": "(user,candidate) scores/sec at history=50,K=32,d=768; AUC parity vs ref",
+        "metric": METRIC,
         "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "warmup": args.warmup, "ms_per_step": round(el32 / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (seeded MIND-large-shaped impressions as news ids over a random news table; "
                 "random-init weights)",
-        "config": {"workload": "config 3 MIND-large shape, news-id input (per step: per-news precompute "
+        "config": {"workload": "config 3 MIND-large shape, news-id input, fp32 (per step: per-news precompute "
                                "over the whole table + scoring)",
                    "history": L, "K": K, "d": D, "Dc": DC, "candidates": C, "news_table": N_NEWS,
                    "impressions_per_gpu_per_step": B, "global_batch": B * world,
+                   "timed_seconds": round(el32, 3),
                    "parallelism": f"dp{world} (impression shards, no data-path collective)"},
-        "roofline": roof, "precompute": pre, "fp32_parity_mode": f32, "dense_rows_kernel": dense,
+        "roofline": roof,
+        "precompute": {"kernel": "news_pre<fp32>", "ms": round(pre32, 4), "flops": pre_fl,
+                       "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
+                       "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
+        "bf16_mode": bf16_mode, "config2": c2, "metric_step": metric_step, "dense_rows_kernel": dense,
         "cpu_baseline": cpu, "auc_parity": auc,
     }
     print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
+def dense_kernel_line(dev, B=32768, steps=5):
+    """The fused dense-row kernel (weights per impression, miner_score) on the same shape, for
+    comparison: pairs/s and its MFMA fraction."""
+    from miner_amd import ops, synthetic
+    imp = synthetic.impressions(36, 0, B, L=L, d=D, C=C, device=dev, dtype=torch.bfloat16)
+    W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
+    pw = ops.pack_weights(W1, Q, W2, dtype=torch.bfloat16)
+    ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / steps
+    tf = flops_per_impression(L, K, D, DC, C) * B / (ms / 1e3) / 1e12
+    del imp
+    return {"kernel": "miner_fused<bf16,full>", "value": round(B * C / (ms / 1e3), 1), "unit": "pairs/s",
+            "ms_per_launch": round(ms, 4), "impressions": B, "tflops": round(tf, 2),
+            "frac_bf16_peak": round(tf / PEAK_BF16_TFLOPS, 4)}
+
+
+# ---------------------------------------------------------------------------------------------
+# config 4: FastFormer user encoder
+# ---------------------------------------------------------------------------------------------
+FF_L, FF_C, FF_H, FF_B = 50, 40, 256, 50000
+
+
+def ff_flops_per_impression(L=FF_L, C=FF_C, H=FF_H):
+    """Algorithmic FLOPs of the FastFormer user encoder + click predictor (model.py:345-545, :322):
+    per layer 6 H x H linears + 2 H -> 16 head projections + the 2 pooled attentions, then the
+    pooler (att_fc1, att_fc2, weighted sum) and C dot products; the MFMA pad of L to 64 excluded."""
+    layer = 6 * 2 * L * H * H + 2 * 2 * L * H * 16 + 2 * 2 * L * H
+    return 2 * layer + 2 * L * H * H + 2 * L * H + 2 * L * H + 2 * C * H
+
+
+def ff_bytes_per_impression(L=FF_L, C=FF_C, H=FF_H, elem=2):
+    """Algorithmic HBM bytes: history + candidate rows, mask, fp32 scores (parameters excluded)."""
+    return (L + C) * H * elem + L + 4 * C
+
+
+def ff_cpu_baseline(seconds: float = 15.0):
+    """FastFormer oracle (torch fp32 CPU restatement of model.py:345-545, :322) on host cores."""
+    from miner_amd import fastformer as ff
+    from miner_amd import synthetic
+    from oracle import fastformer_oracle as ffo
+    hi = host_info()
+    blob = synthetic.fastformer_params(0)
+    params = {n: t.reshape(shp) for (n, shp), t in
+              zip(ff.PARAMS, torch.split(blob, [int(torch.Size(shp).numel()) for _, shp in ff.PARAMS]))}
+    g = torch.Generator().manual_seed(1)
+    bs = 64
+    E = torch.randn(bs, FF_L, FF_H, generator=g) * 0.0625
+    M = torch.rand(bs, FF_L, generator=g) > 0.3
+    Cd = torch.randn(bs, FF_C, FF_H, generator=g) * 0.0625
+    with torch.no_grad():
+        ffo.scores(params, E, M, Cd)
+        pairs, t0, i = 0, time.perf_counter(), 0
+        while True:
+            ffo.scores(params, E, M, Cd)
+            pairs += bs * FF_C
+            i += 1
+            el = time.perf_counter() - t0
+            if el > seconds and i >= 2:
+                break
+    return {"value": round(pairs / el, 1), "unit": "pairs/s", "cores": hi["threads_used"], "kind": "port",
+            "host_cpus": hi["host_cpus"], "cpu_model": hi["cpu_model"],
+            "sample": f"{pairs // FF_C} impressions x {FF_C} candidates (L={FF_L}, hidden {FF_H}), fp32, "
+                      f"batched {bs} impressions/call, {el:.1f}s"}
+
+
+def run_fastformer(args, rank, world, dev):
+    """BASELINE config 4: the FastFormer kernel over FF_B resident impressions per GPU per step."""
+    from miner_amd import fastformer as ff
+    from miner_amd import synthetic
+    B = args.batch or FF_B
+    bf = torch.bfloat16
+    pool = []
+    for p in range(args.pool):
+        start = (rank * args.pool + p) * B
+        g = torch.Generator().manual_seed(1000 + start)
+        lens = torch.randint(0, FF_L + 1, (B,), generator=g)
+        mask = (torch.arange(FF_L)[None, :] >= (FF_L - lens)[:, None]).to(dev)
+        hist = (torch.randn(B, FF_L, FF_H, generator=g) * 0.0625).to(dev, bf)
+        cand = (torch.randn(B, FF_C, FF_H, generator=g) * 0.0625).to(dev, bf)
+        pool.append((hist, mask, cand))
+    blob = synthetic.fastformer_params(0).to(dev)
+    pk16 = ff.pack(blob, bf)
+    pk32 = ff.pack(blob, torch.float32)
+    torch.cuda.synchronize()
+    tm = EventTimer(dev, 1)
+    out = [None]
+
+    def step(i, timed):
+        hist, mask, cand = pool[i % len(pool)]
+        e = tm.step() if timed else None
+        if e:
+            e[0].record(tm.stream)
+        out[0] = ff.score(hist, mask, cand, pk16)
+        if e:
+            e[1].record(tm.stream)
+
+    elapsed = timed_steps(step, args.steps, args.warmup, world, dev)
+    kern_ms = tm.mean_ms(0)
+    assert torch.isfinite(out[0]).all()
+    f32 = None
+    if args.fp32_steps > 0:
+        hist, mask, cand = pool[0]
+        n32 = min(B, 5000)
+        h32, c32, m32 = hist[:n32].float(), cand[:n32].float(), mask[:n32]
+        ff.score(h32, m32, c32, pk32)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(tm.stream)
+        for _ in range(args.fp32_steps):
+            ff.score(h32, m32, c32, pk32)
+        b.record(tm.stream)
+        torch.cuda.synchronize()
+        ms32 = a.elapsed_time(b) / args.fp32_steps
+        f32 = {"value": round(n32 * FF_C / (ms32 / 1e3), 1), "unit": "pairs/s", "ms_per_step": round(ms32, 3),
+               "impressions": n32,
+               "tflops": round(ff_flops_per_impression() * n32 / (ms32 / 1e3) / 1e12, 2)}
+    if rank != 0:
+        return
+    value = B * FF_C * args.steps * world / elapsed
+    fl = ff_flops_per_impression() * B
+    by = ff_bytes_per_impression() * B
+    tflops = fl / (kern_ms / 1e3) / 1e12
+    gbs = by / (kern_ms / 1e3) / 1e9
+    roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": "ff_fused<bf16>",
+            "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4)}
+    roof_hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_launch": by}
+    cpu = ff_cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
+    line = {
+        "metric": "(user,candidate) scores/sec, FastFormer user encoder (config 4)",
+        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (seeded config-4-shaped impressions, random-init weights)",
+        "config": {"workload": "config 4 FastFormer user encoder", "history": FF_L, "hidden": FF_H,
+                   "heads": 16, "layers": 2, "candidates": FF_C, "impressions_per_gpu_per_step": B,
+                   "global_batch": B * world,
+                   "parallelism": f"dp{world} (impression shards, no data-path collective)"},
+        "roofline": roof, "roofline_hbm": roof_hbm, "fp32_parity_mode": f32, "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# config 5: full-corpus ranking
+# ---------------------------------------------------------------------------------------------
 C5_L, C5_K, C5_N, C5_U, C5_TOPK = 200, 64, 200_000, 2048, 100
 
 
@@ -474,7 +627,7 @@ def corpus_cpu_baseline(seconds: float = 10.0):
     oracle/corpus_oracle.py) on host cores: 8 users against news chunks of 4096 until `seconds`."""
     from miner_amd import synthetic
     from oracle import corpus_oracle as co
-    threads = torch.get_num_threads()
+    hi = host_info()
     g = torch.Generator().manual_seed(5)
     U = 8
     news = torch.randn((16384, D), generator=g) / D ** 0.5
@@ -493,7 +646,8 @@ def corpus_cpu_baseline(seconds: float = 10.0):
             el = time.perf_counter() - t0
             if el > seconds and i >= 2:
                 break
-    return {"value": round(pairs / el, 1), "unit": "(user,news) pairs/s", "cores": threads, "kind": "port",
+    return {"value": round(pairs / el, 1), "unit": "(user,news) pairs/s", "cores": hi["threads_used"],
+            "kind": "port", "host_cpus": hi["host_cpus"], "cpu_model": hi["cpu_model"],
             "sample": f"{U} users (history {C5_L}, K={C5_K}, d={D}) encoded and scored against {pairs // U} news "
                       f"rows in chunks of 4096, fp32, {el:.1f}s (top-k selection not included)"}
 
@@ -504,7 +658,7 @@ def run_corpus(args, rank, world, dev):
     ``--batch`` users (default 2048) per GPU and rank them against the table; users shard over
     ranks (weak scaling, no data-path collective)."""
     from miner_amd import corpus, synthetic
-    U = args.batch if args.batch_set else C5_U
+    U = args.batch or C5_U
     dt = torch.float16
     g = torch.Generator(device=dev).manual_seed(5)
     table = (torch.randn((C5_N, D), generator=g, device=dev) / D ** 0.5).to(dt)
@@ -517,47 +671,27 @@ def run_corpus(args, rank, world, dev):
         lens = torch.randint(1, C5_L + 1, (U,), generator=gg, device=dev)
         mask = torch.arange(C5_L, device=dev)[None, :] >= (C5_L - lens)[:, None]
         pool.append((hid, mask))
-    stream = torch.cuda.current_stream(dev)
+    tm = EventTimer(dev, 2)
+    out = [None]
 
-    def step(i, ev=None):
+    def step(i, timed):
         hid, mask = pool[i % len(pool)]
-        if ev is not None:
-            ev[0].record(stream)
+        e = tm.step() if timed else None
+        if e:
+            e[0].record(tm.stream)
         mui, proj = corpus.encode_users(table, mask, pk, his_ids=hid)
-        if ev is not None:
-            ev[1].record(stream)
-        out = corpus.rank_topk(mui, proj, table, C5_TOPK)
-        if ev is not None:
-            ev[2].record(stream)
-        return out
+        if e:
+            e[1].record(tm.stream)
+        out[0] = corpus.rank_topk(mui, proj, table, C5_TOPK)
+        if e:
+            e[2].record(tm.stream)
 
     steps = args.steps if args.steps_set else 5
     warm = args.warmup if args.warmup_set else 1
-    for i in range(warm):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-    t0 = time.perf_counter()
-    for i in range(steps):
-        out = step(i, ev[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
-    rank_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    assert torch.isfinite(out[0]).all()
+    elapsed = timed_steps(step, steps, warm, world, dev)
+    enc_ms, rank_ms = tm.mean_ms(0), tm.mean_ms(1)
+    assert torch.isfinite(out[0][0]).all()
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
         return
     pairs = U * C5_N
     fl = pairs * 4 * C5_K * D            # M = mui·e and Lg = proj·e per (user, news) pair (model.py:127, :213)
@@ -580,160 +714,149 @@ def run_corpus(args, rank, world, dev):
         "cpu_baseline": corpus_cpu_baseline(min(args.cpu_seconds, 10.0)) if (world == 1 and not args.no_cpu) else None,
     }
     print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
-def load_traffic(path):
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        if t.get("workload") == f"L{L}_K{K}_d{D}_Dc{DC}_C{C}_bf16":
-            return t
-    except (OSError, ValueError):
-        pass
-    return None
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="config3", choices=["config3", "config3-dense", "fastformer", "corpus"])
-    ap.add_argument("--batch", type=int, default=None, help="impressions per GPU per step")
-    ap.add_argument("--pool", type=int, default=2, help="distinct resident batches per GPU")
-    ap.add_argument("--fp32-steps", type=int, default=2)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--news-traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_news.json"))
-    ap.add_argument("--no-dense", action="store_true", help="skip the dense-row kernel comparison")
-    args = ap.parse_args()
-    args.batch_set = args.batch is not None
-    args.steps_set = "--steps" in sys.argv
-    args.warmup_set = "--warmup" in sys.argv
-    if args.batch is None:
-        args.batch = 32768
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    if args.workload == "fastformer":
-        return run_fastformer(args, rank, world, dev)
-    if args.workload == "config3":
-        return run_news(args, rank, world, dev)
-    if args.workload == "corpus":
-        return run_corpus(args, rank, world, dev)
-
+# ---------------------------------------------------------------------------------------------
+# the fused dense-row kernel as the workload
+# ---------------------------------------------------------------------------------------------
+def run_dense(args, rank, world, dev):
+    """config 3 with history / candidates given as [B, L, d] / [B, C, d] rows (miner_score: the
+    fused kernel with the weights per impression), bf16."""
     from miner_amd import ops, synthetic
-
-    B = args.batch
+    B = args.batch or 32768
     bf = torch.bfloat16
-    pool = []
-    for p in range(args.pool):
-        start = (rank * args.pool + p) * B      # each rank scores its own shard
-        imp = synthetic.impressions(36, start, B, L=L, d=D, C=C, device=dev, dtype=bf)
-        pool.append(imp)
+    pool = [synthetic.impressions(36, (rank * args.pool + p) * B, B, L=L, d=D, C=C, device=dev, dtype=bf)
+            for p in range(args.pool)]
     W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
-    pw16 = ops.pack_weights(W1, Q, W2, dtype=bf)        # once per model, outside the timed region
-    pw32 = ops.pack_weights(W1, Q, W2, dtype=torch.float32)
-    out = torch.empty((B, C), device=dev, dtype=torch.float32)
-    torch.cuda.synchronize()
+    pw16 = ops.pack_weights(W1, Q, W2, dtype=bf)
+    tm = EventTimer(dev, 1)
+    out = [None]
 
-    def step(i):
+    def step(i, timed):
         imp = pool[i % len(pool)]
-        return ops.score(imp.history, imp.his_mask, imp.candidates, pw16)
+        e = tm.step() if timed else None
+        if e:
+            e[0].record(tm.stream)
+        out[0] = ops.score(imp.history, imp.his_mask, imp.candidates, pw16)
+        if e:
+            e[1].record(tm.stream)
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        out = step(i)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    assert torch.isfinite(out).all()
-
-    # fp32 parity mode on the same impressions (fewer steps: it runs at the fp32 MFMA rate)
-    f32 = None
-    if args.fp32_steps > 0:
-        imp = pool[0]
-        h32, c32 = imp.history.float(), imp.candidates.float()
-        ops.score(h32, imp.his_mask, c32, pw32)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(args.fp32_steps):
-            ops.score(h32, imp.his_mask, c32, pw32)
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms32 = a.elapsed_time(b) / args.fp32_steps
-        f32 = {"value": round(B * C / (ms32 / 1e3), 1), "unit": "pairs/s", "ms_per_step": round(ms32, 3),
-               "tflops": round(flops_per_impression(L, K, D, DC, C) * B / (ms32 / 1e3) / 1e12, 2),
-               "frac_fp32_peak": round(flops_per_impression(L, K, D, DC, C) * B / (ms32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)}
-        del h32, c32
-
+    elapsed = timed_steps(step, args.steps, args.warmup, world, dev)
+    kern_ms = tm.mean_ms(0)
+    assert torch.isfinite(out[0]).all()
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
         return
-
-    pairs_total = B * C * args.steps * world
-    value = pairs_total / elapsed
     fl = flops_per_impression(L, K, D, DC, C) * B
     by = bytes_per_impression(L, D, C, 2) * B
     tflops = fl / (kern_ms / 1e3) / 1e12
     gbs = by / (kern_ms / 1e3) / 1e9
-    traffic = load_traffic(args.traffic)
-    traffic_bytes, mfma_busy = None, None
-    if traffic and traffic.get("batch") == B:
-        traffic_bytes = traffic.get("hbm_bytes_per_launch")
-        mfma_busy = traffic.get("mfma_busy_frac")
-    roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic_bytes,
-            "kernel": "miner_fused<bf16,full>", "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4),
-            "mfma_busy_pmc": mfma_busy}
-    roof_hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_launch": by,
-                "traffic": traffic_bytes}
-    cpu = None
-    if world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_seconds)
+    pmc = load_pmc(args.traffic, f"L{L}_K{K}_d{D}_Dc{DC}_C{C}_bf16", B)
     line = {
-        "metric": "(user,candidate) scores/sec at history=50,K=32,d=768; AUC parity vs ref",
-        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "metric": METRIC, "value": round(B * C * args.steps * world / elapsed, 1), "unit": "pairs/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (seeded MIND-large-shaped impressions, random-init weights)",
-        "config": {"workload": "config 3 MIND-large shape", "history": L, "K": K, "d": D, "Dc": DC,
+        "config": {"workload": "config 3 MIND-large shape, dense rows", "history": L, "K": K, "d": D, "Dc": DC,
                    "candidates": C, "impressions_per_gpu_per_step": B, "global_batch": B * world,
                    "parallelism": f"dp{world} (impression shards, no data-path collective)"},
-        "roofline": roof, "roofline_hbm": roof_hbm, "fp32_parity_mode": f32, "cpu_baseline": cpu,
+        "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / PEAK_BF16_TFLOPS, 4),
+                     "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                     "kernel": "miner_fused<bf16,full>", "flops_per_launch": fl, "kernel_ms": round(kern_ms, 4),
+                     "mfma_busy_pmc": pmc.get("mfma_busy_frac") if pmc else None},
+        "roofline_hbm": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_launch": by},
+        "cpu_baseline": cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None,
     }
     print(json.dumps(line), flush=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# launcher and dry run
+# ---------------------------------------------------------------------------------------------
+def run_dry(args, rank, world, dev):
+    """The launcher + timing protocol without a GPU (gloo): a step is a small CPU matmul."""
+    a = torch.randn(64, 64)
+
+    def step(i, timed):
+        torch.mm(a, a)
+
+    elapsed = timed_steps(step, args.steps, args.warmup, world, dev)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(64 * args.steps * world / elapsed, 1), "unit": "pairs/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "dry run (no kernel)",
+                          "config": {"workload": "dry run: launcher and timing protocol only"}}), flush=True)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """--gpus N without a torch.distributed environment: start N ranks as CHILD processes (the
+    torch.distributed.run launcher, one process per GPU) before anything touches the GPU, and exit
+    with their status — never an exec from this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="config3", choices=["config3", "config3-dense", "fastformer", "corpus"])
+    ap.add_argument("--batch", type=int, default=None, help="impressions (users) per GPU per step")
+    ap.add_argument("--pool", type=int, default=2, help="distinct resident batches per GPU")
+    ap.add_argument("--fp32-steps", type=int, default=2, help="(fastformer) fp32 parity-mode launches")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-dense", action="store_true", help="skip the dense-row kernel comparison")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 sub-line")
+    ap.add_argument("--no-metrics", action="store_true", help="skip the device metric step")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--news-traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_news.json"))
+    ap.add_argument("--news-traffic32", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_fp32.json"))
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo: launcher and timing protocol only")
+    args = ap.parse_args()
+    args.steps_set = "--steps" in sys.argv
+    args.warmup_set = "--warmup" in sys.argv
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        return launch_ranks(args.gpus)
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        run_dry(args, rank, world, dev)
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+        {"config3": run_news, "config3-dense": run_dense, "fastformer": run_fastformer,
+         "corpus": run_corpus}[args.workload](args, rank, world, dev)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -5,7 +5,7 @@
  * (src/evaluation.py:36-84 BaseEvaluator.compute_scores with compute_mrr_score :177-192,
  * compute_dcg_score / compute_ndcg_score :195-231, is_hit :245-249 and sklearn's roc_auc_score for
  * group_auc :56-61), which the reference runs as a Python loop (~0.9 ms per impression). The
- * flattened global `auc` (:53-55) is not per-impression and stays with the caller.
+ * flattened global `auc` (:53-55) is not per-impression: miner_global_auc computes it on the device.
  *
  * Conventions as in miner_score.h: caller-owned device memory, asynchronous on `stream`.
  */
@@ -37,6 +37,19 @@ extern "C" {
 int miner_impression_metrics(void* stream, const float* scores, const uint8_t* labels,
                              const int32_t* offsets, int G, const int32_t* ks, int nk,
                              double* out, uint8_t* mixed_ties);
+
+/*
+ * The flattened global `auc` of the reference (src/evaluation.py:53-55: sklearn roc_auc_score over
+ * every (label, probability) pair of the eval set), exactly, on the device: a radix sort of the
+ * scores (hipCUB), a reduce-by-key over runs of equal scores and an integer Mann-Whitney sum with
+ * ties counted 1/2.  n <= 2^31 - 1 pairs; `scores` fp32, `labels` uint8 0/1 (device memory);
+ * `workspace` caller-owned device memory of at least miner_auc_workspace_bytes(n) bytes (about
+ * 33 bytes per pair); `auc_out` one float64 in DEVICE memory, NaN when one class is absent
+ * (sklearn raises there).
+ */
+size_t miner_auc_workspace_bytes(int64_t n);
+int miner_global_auc(void* stream, const float* scores, const uint8_t* labels, int64_t n, void* workspace,
+                     size_t workspace_bytes, double* auc_out);
 
 #ifdef __cplusplus
 }

@@ -76,6 +76,13 @@ int miner_pack_weights(void* stream, int dtype, const void* w_poly, const void* 
                        const void* w_target, int d, int Dc, int K, void* packed);
 
 /*
+ * TargetAwareAttention.linear.weight [d, d] alone (model.py:198), for miner_target_aware with
+ * Dc = 0: the W2 part of the miner_pack_weights layout, miner_target_weights_bytes() bytes.
+ */
+size_t miner_target_weights_bytes(int dtype, int d);
+int miner_pack_target_weights(void* stream, int dtype, const void* w_target, int d, void* packed);
+
+/*
  * Score B impressions.
  *   history      [B, L, d]  dtype  clicked-news embeddings, left-padded (reader.py:369)
  *   his_mask     [B, L]     uint8  1 = real click, 0 = pad (entities.py:395)
@@ -116,7 +123,8 @@ int miner_score_gather(void* stream, int dtype, int score_type, const void* news
  * TargetAwareAttention.forward (model.py:200-216) on its own:
  *   query [B, K, d] dtype (multi_user_interest), key [sum C_b, d] dtype (candidates),
  *   value [sum C_b, K] fp32 (matching scores Cand·muiᵀ), packed_weights with w_target packed
- *   (Dc = the context-code dim they were packed with) -> out [sum C_b] fp32.
+ *   (Dc = the context-code dim they were packed with, or 0 for a miner_pack_target_weights
+ *   buffer) -> out [sum C_b] fp32.
  */
 int miner_target_aware(void* stream, int dtype,
                        const void* query, const void* key, const float* value,

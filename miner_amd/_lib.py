@@ -27,6 +27,8 @@ SIGNATURES = {
     "miner_score": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "miner_score_gather": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "miner_target_aware": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "miner_target_weights_bytes": (ctypes.c_size_t, [_I, _I]),
+    "miner_pack_target_weights": (_I, [_P, _I, _P, _I, _P]),
     "miner_supported": (_I, [_I, _I, _I, _I, _I]),
     "miner_lds_bytes": (_I, [_I, _I, _I, _I, _I]),
     "miner_strerror": (ctypes.c_char_p, [_I]),
@@ -48,6 +50,8 @@ SIGNATURES = {
     "miner_news_supported": (_I, [_I, _I, _I, _I, _I]),
     # include/miner_metrics.h
     "miner_impression_metrics": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
+    "miner_auc_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "miner_global_auc": (_I, [_P, _P, _P, ctypes.c_int64, _P, ctypes.c_size_t, _P]),
 }
 
 _lib = None

@@ -16,7 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "miner_score.hip")      # the fused scoring kernel
 SOURCES = [SRC, os.path.join(HERE, "csrc", "miner_metrics.hip"), os.path.join(HERE, "csrc", "fastformer.hip"),
-           os.path.join(HERE, "csrc", "corpus.hip"), os.path.join(HERE, "csrc", "news.hip")]
+           os.path.join(HERE, "csrc", "corpus.hip"), os.path.join(HERE, "csrc", "news.hip"),
+           os.path.join(HERE, "csrc", "miner_auc.hip")]
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("miner_score.h", "miner_metrics.h", "miner_fastformer.h", "miner_corpus.h", "miner_news.h")] + [os.path.join(HERE, "csrc", "cdna4_common.h")]
 LIB = os.path.join(HERE, "libminer_hip.so")
 ARCH = os.environ.get("MINER_OFFLOAD_ARCH", "gfx950")
@@ -32,25 +33,55 @@ def hipcc() -> str:
 DEBUG_LIB = os.path.join(HERE, "libminer_hip_dbg.so")
 
 
-def build_library(force: bool = False, verbose: bool = False, debug: bool = False) -> str:
+def _objdir(debug: bool) -> str:
+    return os.path.join(ROOT, "build", "obj_dbg" if debug else "obj")
+
+
+def build_library(force: bool = False, verbose: bool = False, debug: bool = False, jobs: int = None) -> str:
     """Compile csrc/*.hip -> miner_amd/libminer_hip.so (skipped when up to date).
+
+    Each translation unit is compiled to its own object in parallel (non-rdc HIP: every object
+    carries and registers its own gfx950 code object), then linked; an object is rebuilt when its
+    source or any shared header is newer.
 
     ``debug`` builds the diagnostic variant libminer_hip_dbg.so instead (-DMINER_NEWS_DEBUG:
     every DMA / store address of the news kernel is range-checked and violations are printed;
     load it with MINER_HIP_LIB=miner_amd/libminer_hip_dbg.so)."""
+    from concurrent.futures import ThreadPoolExecutor
     lib = DEBUG_LIB if debug else LIB
     deps = SOURCES + HEADERS
     if not force and os.path.exists(lib) and all(os.path.getmtime(lib) >= os.path.getmtime(p) for p in deps):
         return lib
+    od = _objdir(debug)
+    os.makedirs(od, exist_ok=True)
+    hdr_t = max(os.path.getmtime(h) for h in HEADERS)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed",
+             *(["-DMINER_NEWS_DEBUG"] if debug else []), "-I", os.path.join(ROOT, "include")]
+
+    def compile_one(src):
+        obj = os.path.join(od, os.path.basename(src)[:-4] + ".o")
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_t):
+            return obj
+        tmp = obj + f".tmp{os.getpid()}"
+        cmd = [hipcc(), *flags, "-c", src, "-o", tmp]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {os.path.basename(src)} ({res.returncode}):\n{res.stderr[-4000:]}")
+        os.replace(tmp, obj)
+        return obj
+
+    jobs = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 4) // 2))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = lib + f".tmp{os.getpid()}"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-pass-failed", *(["-DMINER_NEWS_DEBUG"] if debug else []),
-           "-I", os.path.join(ROOT, "include"), *SOURCES, "-o", tmp]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+        raise RuntimeError(f"link failed ({res.returncode}):\n{res.stderr[-4000:]}")
     os.replace(tmp, lib)
     return lib
 

@@ -1095,6 +1095,30 @@ int miner_pack_weights(void* stream, int dtype, const void* w_poly, const void* 
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
+size_t miner_target_weights_bytes(int dtype, int d) {
+  if ((dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) || d <= 0 || d % 32 || d > kMaxD) return 0;
+  return w2p_elems(d) * (dtype == MINER_DTYPE_BF16 ? 2 : 4);
+}
+
+// W2 alone (TargetAwareAttention.linear.weight, model.py:198) in the tiled layout: the packed
+// buffer of miner_pack_weights with an empty PolyAttention part (Dc = 0), for miner_target_aware
+int miner_pack_target_weights(void* stream, int dtype, const void* w_target, int d, void* packed) {
+  if (dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) return MINER_EINVAL;
+  if (d <= 0 || !w_target || !packed) return MINER_EINVAL;
+  if (d % 32 || d > kMaxD) return MINER_ESHAPE;
+  if (!aligned16(packed)) return MINER_EALIGN;
+  const size_t n = w2p_elems(d);
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  if (dtype == MINER_DTYPE_BF16)
+    hipLaunchKernelGGL(pack_weights_kernel<__bf16>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       nullptr, nullptr, static_cast<const __bf16*>(w_target), d, 0, 0, static_cast<__bf16*>(packed));
+  else
+    hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       nullptr, nullptr, static_cast<const float*>(w_target), d, 0, 0, static_cast<float*>(packed));
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
 int miner_score(void* stream, int dtype, int score_type, const void* history, const uint8_t* his_mask,
                 const float* his_bias, const void* candidates, const int32_t* cand_offsets,
                 const void* packed_weights, int B, int L, int C, int d, int Dc, int K, float* scores,
@@ -1141,7 +1165,7 @@ int miner_score_gather(void* stream, int dtype, int score_type, const void* news
 int miner_target_aware(void* stream, int dtype, const void* query, const void* key, const float* value,
                        const int32_t* cand_offsets, const void* packed_weights, int Dc, int B, int C, int d, int K,
                        float* out) {
-  if (B < 0 || C < 0 || Dc <= 0) return MINER_EINVAL;
+  if (B < 0 || C < 0 || Dc < 0) return MINER_EINVAL;     // Dc = 0: a miner_pack_target_weights buffer
   const int sh = check_shape(dtype, kTaa, 1, d, 1, K);
   if (sh != MINER_OK) return sh;
   if (!query || !key || !value || !packed_weights || !out) return MINER_EINVAL;

@@ -6,8 +6,9 @@ evaluation needs exchanges, and only small ones:
 
 * group_auc / mrr / ndcg@k / hit@k are ``np.nanmean`` over impressions (src/evaluation.py:56-82):
   each rank all-reduces (Σ non-NaN values, count) — a few float64s per metric;
-* the global ``auc`` (src/evaluation.py:53-55) is not decomposable: every rank all-gathers the
-  (score, label) pairs and computes the exact AUC (c3: 120 M pairs ≈ 600 MB, sub-second over xGMI);
+* the global ``auc`` (src/evaluation.py:53-55) is not decomposable: the (score, label) pairs are
+  gathered once to rank 0 (c3: 120 M pairs ≈ 600 MB over xGMI), which computes the exact AUC on its
+  device (miner_global_auc) and broadcasts it;
 * the eval loss (src/loss.py:68-85, src/trainer.py:276-291) is a sum of per-sample terms once the
   batch partition is fixed: all-reduce (numerator, positives).
 
@@ -92,6 +93,37 @@ def all_gather_concat(x: torch.Tensor) -> torch.Tensor:
     return torch.cat([o[:s] for o, s in zip(out, sizes)])
 
 
+def gather_concat_to_root(x: torch.Tensor, root: int = 0):
+    """Concatenate every rank's 1-D tensor in rank order on ``root`` only (None elsewhere; identity
+    on one process). One gather of max-size padded buffers: the data crosses the links once."""
+    if world()[1] == 1:
+        return x
+    dev = _coll_device()
+    x = x.to(dev).contiguous()
+    n = torch.tensor([x.numel()], device=dev, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(dist.get_world_size())]
+    dist.all_gather(sizes, n)
+    sizes = [int(s) for s in sizes]
+    m = max(sizes)
+    buf = torch.zeros(m, device=dev, dtype=x.dtype)
+    buf[:x.numel()] = x
+    if dist.get_rank() == root:
+        out = [torch.empty_like(buf) for _ in sizes]
+        dist.gather(buf, out, dst=root)
+        return torch.cat([o[:s] for o, s in zip(out, sizes)])
+    dist.gather(buf, None, dst=root)
+    return None
+
+
+def broadcast_float(v, root: int = 0) -> float:
+    """One float64 from ``root`` to every rank."""
+    if world()[1] == 1:
+        return float(v)
+    t = torch.tensor([float("nan") if v is None else float(v)], dtype=torch.float64, device=_coll_device())
+    dist.broadcast(t, src=root)
+    return float(t.item())
+
+
 def reduce_metrics(pairs: "evaluation.GroupedPairs", metrics: List[str], save_result: bool = False,
                    path: str = None) -> Dict[str, float]:
     """The reference's compute_scores (src/evaluation.py:36-84) over all ranks' impressions.
@@ -106,17 +138,19 @@ def reduce_metrics(pairs: "evaluation.GroupedPairs", metrics: List[str], save_re
     out = {}
     for metric in metrics:
         if metric == "auc":
-            sc = all_gather_concat(torch.from_numpy(pairs.scores))
-            lb = all_gather_concat(torch.from_numpy(pairs.labels.astype(np.uint8)))
-            out["auc"] = evaluation.auc_score(lb.cpu().numpy(), sc.cpu().numpy())
+            sc = gather_concat_to_root(torch.from_numpy(pairs.scores))
+            lb = gather_concat_to_root(torch.from_numpy(pairs.labels.astype(np.uint8)))
+            auc = evaluation.auc_score(lb.cpu().numpy(), sc.cpu().numpy()) if rank == 0 else None
+            out["auc"] = broadcast_float(auc)
             continue
         vals = pairs.per_impression(metric)
         ok = ~np.isnan(vals)
         s, c = all_reduce_sum(np.array([vals[ok].sum(), ok.sum()], np.float64))
         out[evaluation.metric_key(metric)] = float(s / c) if c > 0 else float("nan")
         if save_result:
-            full = all_gather_concat(torch.from_numpy(vals)).cpu().numpy()
+            full = gather_concat_to_root(torch.from_numpy(vals))
             if rank == 0:
+                full = full.cpu().numpy()
                 w = full.astype(int) if metric.startswith("hit") else full
                 evaluation.save_scores(os.path.join(path, evaluation.metric_file(metric)), w.tolist())
     return out
@@ -132,17 +166,21 @@ def reduce_device_metrics(probs: torch.Tensor, labels: torch.Tensor, offsets: to
     out = {}
     for metric in metrics:
         if metric == "auc":
-            sc = all_gather_concat(probs.double().reshape(-1))
-            lb = all_gather_concat(labels.reshape(-1).to(torch.uint8))
-            out["auc"] = evaluation.auc_score(lb.cpu().numpy(), sc.cpu().numpy())
+            # exact global AUC (evaluation.py:53-55): the pairs go to rank 0 once, the device rank
+            # sum runs there (miner_global_auc), the value is broadcast
+            sc = gather_concat_to_root(probs.float().reshape(-1))
+            lb = gather_concat_to_root(labels.reshape(-1).to(torch.uint8))
+            auc = gm.global_auc(sc.to(probs.device), lb.to(probs.device)) if rank == 0 else None
+            out["auc"] = broadcast_float(auc)
             continue
         vals = per[metric]
         ok = ~np.isnan(vals)
         s, c = all_reduce_sum(np.array([vals[ok].sum(), ok.sum()], np.float64))
         out[evaluation.metric_key(metric)] = float(s / c) if c > 0 else float("nan")
         if save_result:
-            full = all_gather_concat(torch.from_numpy(vals)).cpu().numpy()
+            full = gather_concat_to_root(torch.from_numpy(vals))
             if rank == 0:
+                full = full.cpu().numpy()
                 w = full.astype(int) if metric.startswith("hit") else full
                 evaluation.save_scores(os.path.join(path, evaluation.metric_file(metric)), w.tolist())
     return out

@@ -69,6 +69,32 @@ def per_impression(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: Sequ
     return {m: cols[evaluation.metric_key(m)] for m in metrics if m != "auc"}
 
 
+def global_auc(probs: Tensor, labels: Tensor) -> float:
+    """The reference's flattened ``auc`` (src/evaluation.py:53-55, sklearn roc_auc_score over all
+    pairs) computed exactly on the device (``miner_global_auc``: radix sort + integer rank sum, ties
+    counted one half). NaN when a class is absent (where sklearn raises)."""
+    for t in (probs, labels):
+        if t.device.type != "cuda":
+            raise RuntimeError("miner_amd.metrics runs on the GPU only (no CPU fallback)")
+    p = probs.reshape(-1).to(torch.float32).contiguous()
+    y = labels.reshape(-1).to(device=p.device, dtype=torch.uint8).contiguous()
+    n = p.numel()
+    if n != y.numel():
+        raise ValueError(f"{n} scores but {y.numel()} labels")
+    if n == 0:
+        return float("nan")
+    nbytes = _lib.lib().miner_auc_workspace_bytes(n)
+    if nbytes == 0:
+        raise ValueError(f"global AUC over {n} pairs is not supported (at most 2^31 - 1)")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=p.device)
+    out = torch.empty(1, dtype=torch.float64, device=p.device)
+    with torch.cuda.device(p.device):
+        rc = _lib.lib().miner_global_auc(torch.cuda.current_stream(p.device).cuda_stream, p.data_ptr(), y.data_ptr(),
+                                         n, ws.data_ptr(), nbytes, out.data_ptr())
+    _lib.check(rc, "miner_global_auc")
+    return float(out.item())
+
+
 def compute_metrics(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: List[str], save_result: bool = False,
                     path: str = None) -> Dict[str, float]:
     """The reference's metric dict (src/evaluation.py:36-84) for impressions already sorted by id."""
@@ -76,7 +102,7 @@ def compute_metrics(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: Lis
     out = {}
     for m in metrics:
         if m == "auc":
-            out["auc"] = evaluation.auc_score(labels.reshape(-1).cpu().numpy(), probs.reshape(-1).double().cpu().numpy())
+            out["auc"] = global_auc(probs, labels)
             continue
         vals = per[m]
         out[evaluation.metric_key(m)] = float(np.nanmean(vals))
@@ -109,6 +135,10 @@ class DeviceEvaluator:
         self._ids.append(impression_ids.reshape(-1).to(device=scores.device, dtype=torch.int64))
 
     def arrays(self):
+        if not self._probs:           # an empty shard (a rank with no impressions)
+            dev = torch.device("cuda", torch.cuda.current_device())
+            return (torch.zeros(0, device=dev), torch.zeros(0, dtype=torch.uint8, device=dev),
+                    torch.zeros(1, dtype=torch.int32, device=dev))
         probs = torch.cat(self._probs)
         lab = torch.cat(self._labels)
         sizes = torch.cat(self._sizes)
@@ -126,5 +156,7 @@ class DeviceEvaluator:
         from . import distributed
         probs, lab, offs = self.arrays()
         if distributed.world()[1] == 1:
+            if offs.numel() == 1:
+                raise ValueError("no impressions to evaluate")
             return compute_metrics(probs, lab, offs, metrics, save_result, path)
         return distributed.reduce_device_metrics(probs, lab, offs, metrics, save_result, path)

@@ -46,16 +46,20 @@ class _PackCache:
     def __init__(self):
         self._c = {}
 
-    def get(self, dtype: torch.dtype, w_poly: Tensor, context_codes: Tensor, w_target: Tensor = None):
+    def get(self, dtype: torch.dtype, w_poly: Tensor = None, context_codes: Tensor = None, w_target: Tensor = None):
+        """Packed weights for (W1, Q[, W2]), or W2 alone when w_poly is None (TargetAwareAttention)."""
         params = [t for t in (w_poly, context_codes, w_target) if t is not None]
-        key = (dtype, w_poly.device)
+        key = (dtype, params[0].device)
         stamp = tuple((t._version, t.data_ptr()) for t in params)
         hit = self._c.get(key)
         if hit is not None and hit[0] == stamp:
             return hit[1]
         with torch.no_grad():
-            packed = ops.pack_weights(w_poly.detach(), context_codes.detach(),
-                                      None if w_target is None else w_target.detach(), dtype=dtype)
+            if w_poly is None:
+                packed = ops.pack_target_weights(w_target.detach(), dtype=dtype)
+            else:
+                packed = ops.pack_weights(w_poly.detach(), context_codes.detach(),
+                                          None if w_target is None else w_target.detach(), dtype=dtype)
         self._c[key] = (stamp, packed)
         return packed
 
@@ -92,11 +96,7 @@ class TargetAwareAttention(nn.Module):
     def forward(self, query: Tensor, key: Tensor, value: Tensor) -> Tensor:
         """query [B,K,d], key [B,C,d], value [B,C,K] -> [B,C] fp32."""
         dt = _PREC[self.precision]
-        K, d = query.shape[1], query.shape[2]
-        if getattr(self, "_dummy", None) is None or self._dummy[0].shape != (32, d) or self._dummy[1].shape[0] != K \
-                or self._dummy[0].device != query.device:
-            self._dummy = (torch.zeros((32, d), device=query.device), torch.zeros((K, 32), device=query.device))
-        packed = self._pc.get(dt, self._dummy[0], self._dummy[1], self.linear.weight)
+        packed = self._pc.get(dt, w_target=self.linear.weight)          # W2 alone (model.py:198)
         return ops.target_aware(query.to(dt), key.to(dt), value, packed)
 
 

@@ -92,6 +92,41 @@ def pack_weights(w_poly: torch.Tensor, context_codes: torch.Tensor, w_target: to
     return PackedWeights(buf, dtype, d, Dc, K, w2 is not None)
 
 
+def pack_target_weights(w_target: torch.Tensor, dtype: torch.dtype | None = None) -> PackedWeights:
+    """Pack target_aware_attn.linear.weight [d,d] (model.py:198) alone, for ``target_aware``
+    (TargetAwareAttention on its own has no PolyAttention weights: Dc = K = 0 in the result)."""
+    _require_device(w_target)
+    dtype = dtype or w_target.dtype
+    dt = _dtype_code(dtype)
+    w2 = _contig(w_target, dtype)
+    if w2.dim() != 2 or w2.shape[0] != w2.shape[1]:
+        raise ValueError(f"w_target must be [d,d], got {tuple(w2.shape)}")
+    d = w2.shape[0]
+    nbytes = _lib.lib().miner_target_weights_bytes(dt, d)
+    if nbytes == 0:
+        raise ValueError(f"w_target d={d} not supported by this build (d % 32 == 0, d <= 1024)")
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=w2.device)
+    with torch.cuda.device(w2.device):
+        rc = _lib.lib().miner_pack_target_weights(_stream(w2.device), dt, _ptr(w2), d, _ptr(buf))
+    _lib.check(rc, "miner_pack_target_weights")
+    return PackedWeights(buf, dtype, d, 0, 0, True)
+
+
+def _check_mask_bias(his_mask: torch.Tensor, his_bias, B: int, L: int):
+    """his_mask [B,L] (bool or 0/1) -> contiguous uint8 view; his_bias [B,L] fp32 or None."""
+    mask = _contig(his_mask)
+    if mask.dtype != torch.bool:
+        mask = mask != 0
+    if tuple(mask.shape) != (B, L):
+        raise ValueError(f"his_mask must be [{B},{L}], got {tuple(mask.shape)}")
+    if his_bias is not None:
+        his_bias = _contig(his_bias, torch.float32)
+        if tuple(his_bias.shape) != (B, L):
+            raise ValueError(f"his_bias must be [{B},{L}] (category bias averaged over candidates), "
+                             f"got {tuple(his_bias.shape)}")
+    return mask.view(torch.uint8), his_bias
+
+
 def _as_packed(w_poly, context_codes, w_target, dtype) -> PackedWeights:
     if isinstance(w_poly, PackedWeights):
         if w_poly.dtype != dtype:
@@ -137,18 +172,11 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
     pw = _as_packed(w_poly, context_codes, w_target if st == _lib.SCORE_WEIGHTED else None, tdt)
     if pw.d != d:
         raise ValueError(f"packed weights are for d={pw.d}, history has d={d}")
+    if pw.Dc == 0:
+        raise ValueError("packed weights hold no PolyAttention part (pack_target_weights output)")
     if st == _lib.SCORE_WEIGHTED and not pw.has_target:
         raise ValueError("score_type='weighted' needs weights packed with w_target")
-    mask = _contig(his_mask)
-    if mask.dtype != torch.bool:
-        mask = mask != 0
-    if tuple(mask.shape) != (B, L):
-        raise ValueError(f"his_mask must be [{B},{L}]")
-    mask = mask.view(torch.uint8)
-    if his_bias is not None:
-        his_bias = _contig(his_bias, torch.float32)
-        if tuple(his_bias.shape) != (B, L):
-            raise ValueError(f"his_bias must be [{B},{L}] (category bias averaged over candidates)")
+    mask, his_bias = _check_mask_bias(his_mask, his_bias, B, L)
     if cand_offsets is None:
         if candidates.dim() != 3 or candidates.shape[0] != B or candidates.shape[2] != d:
             raise ValueError(f"dense candidates must be [{B},C,{d}]")
@@ -208,17 +236,16 @@ def score_gather(news_table: torch.Tensor, his_ids: torch.Tensor, his_mask: torc
     code = _lib.lib().miner_supported(dt, L, d, Dc, K)
     if code != 0:
         raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
+    if st == _lib.SCORE_WEIGHTED and not isinstance(w_poly, PackedWeights) and w_target is None:
+        raise ValueError("score_type='weighted' needs w_target (target_aware_attn.linear.weight)")
     pw = _as_packed(w_poly, context_codes, w_target if st == _lib.SCORE_WEIGHTED else None, tdt)
+    if pw.d != d:
+        raise ValueError(f"packed weights are for d={pw.d}, the news table has d={d}")
+    if pw.Dc == 0:
+        raise ValueError("packed weights hold no PolyAttention part (pack_target_weights output)")
     if st == _lib.SCORE_WEIGHTED and not pw.has_target:
         raise ValueError("score_type='weighted' needs weights packed with w_target")
-    mask = _contig(his_mask)
-    if mask.dtype != torch.bool:
-        mask = mask != 0
-    if tuple(mask.shape) != (B, L):
-        raise ValueError(f"his_mask must be [{B},{L}]")
-    mask = mask.view(torch.uint8)
-    if his_bias is not None:
-        his_bias = _contig(his_bias, torch.float32)
+    mask, his_bias = _check_mask_bias(his_mask, his_bias, B, L)
     if cand_offsets is None:
         if cand_ids.dim() != 2 or cand_ids.shape[0] != B:
             raise ValueError(f"dense cand_ids must be [{B},C]")
@@ -253,14 +280,13 @@ def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly, contex
     dt = _dtype_code(tdt)
     history = _contig(history)
     pw = _as_packed(w_poly, context_codes, None, tdt)
+    if history.dim() != 3:
+        raise ValueError(f"history must be [B,L,d], got {tuple(history.shape)}")
     B, L, d = history.shape
     Dc, K = pw.Dc, pw.K
-    mask = _contig(his_mask)
-    if mask.dtype != torch.bool:
-        mask = mask != 0
-    mask = mask.view(torch.uint8)
-    if his_bias is not None:
-        his_bias = _contig(his_bias, torch.float32)
+    if pw.d != d or Dc == 0:
+        raise ValueError(f"packed weights are for d={pw.d} (Dc={Dc}), history has d={d}")
+    mask, his_bias = _check_mask_bias(his_mask, his_bias, B, L)
     code = _lib.lib().miner_supported(dt, L, d, Dc, K)
     if code != 0:
         raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
@@ -285,16 +311,22 @@ def target_aware(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, w_
     query = _contig(query)
     key = _contig(key, tdt)
     value = _contig(value, torch.float32)
+    if query.dim() != 3:
+        raise ValueError(f"query must be [B,K,d], got {tuple(query.shape)}")
     B, K, d = query.shape
     if isinstance(w_target, PackedWeights):
         pw = w_target
         if not pw.has_target or pw.dtype != tdt:
             raise ValueError("packed weights must hold w_target in the query dtype")
+        if pw.d != d:
+            raise ValueError(f"packed w_target is for d={pw.d}, query has d={d}")
+        if pw.K and pw.K != K:
+            raise ValueError(f"packed weights are for K={pw.K}, query has K={K}")
     else:
         _require_device(w_target)
-        # TAA alone needs only W2; pack it with a trivial (zero) PolyAttention block
-        pw = pack_weights(torch.zeros((32, d), device=query.device, dtype=tdt),
-                          torch.zeros((K, 32), device=query.device, dtype=tdt), w_target, dtype=tdt)
+        if tuple(w_target.shape) != (d, d):
+            raise ValueError(f"w_target must be [{d},{d}], got {tuple(w_target.shape)}")
+        pw = pack_target_weights(w_target, dtype=tdt)          # TAA alone needs only W2
     if cand_offsets is None:
         C = key.shape[1]
         if tuple(key.shape) != (B, C, d) or tuple(value.shape) != (B, C, K):
@@ -302,6 +334,8 @@ def target_aware(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, w_
         out = torch.empty((B, C), device=query.device, dtype=torch.float32)
         offs = None
     else:
+        if key.dim() != 2 or key.shape[1] != d or tuple(value.shape) != (key.shape[0], K):
+            raise ValueError("ragged key must be [N,d] and value [N,K]")
         offs = _contig(cand_offsets, torch.int32)
         if validate_offsets:
             check_offsets(offs, B, key.shape[0])
