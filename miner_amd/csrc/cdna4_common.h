@@ -154,6 +154,32 @@ __device__ __forceinline__ f32x16 zero16() {
 // torch.nn.functional.gelu(approximate='none')
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
 
+// The same GELU branch-free for the fp32 parity kernels: x·Φ(x) with Φ from the Chebyshev erfc of
+// Numerical Recipes (erfc(z) = t·exp(-z² + P(t)), t = 1/(1 + z/2), fractional error < 1.2e-7 for
+// every z >= 0, tails included): Φ(x) = erfc(|x|/√2)/2 for x < 0, 1 - erfc(|x|/√2)/2 otherwise.
+// |Δgelu| <= 1.6e-7·max(1, |x|) against float64 (tools/gelu_error.py; hardware rcp / exp2 add ~1 ulp)
+// — about the rounding of Φ itself — in ~16 VALU with one v_rcp and one v_exp, where libm erff
+// runs two divergent polynomial branches (~40 VALU + exec-mask SALU). The fp32 MFMA does not
+// co-issue with VALU on gfx950, so every VALU instruction of the GELU is paid in MFMA time.
+__device__ __forceinline__ float gelu_erfc_nr(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.5f, z, 1.0f));
+  float q = 0.17087277f;
+  q = __builtin_fmaf(q, t, -0.82215223f);
+  q = __builtin_fmaf(q, t, 1.48851587f);
+  q = __builtin_fmaf(q, t, -1.13520398f);
+  q = __builtin_fmaf(q, t, 0.27886807f);
+  q = __builtin_fmaf(q, t, -0.18628806f);
+  q = __builtin_fmaf(q, t, 0.09678418f);
+  q = __builtin_fmaf(q, t, 0.37409196f);
+  q = __builtin_fmaf(q, t, 1.00002368f);
+  q = __builtin_fmaf(q, t, -1.26551223f);
+  const float y = __builtin_fmaf(-z, z, q);
+  const float ec = t * __builtin_amdgcn_exp2f(y * 1.4426950408889634f);   // erfc(z)
+  const float phi = x < 0.f ? 0.5f * ec : __builtin_fmaf(-0.5f, ec, 1.0f);
+  return x * phi;
+}
+
 // bf16-mode transcendentals: branch-free, a handful of VALU ops each.  Their error (tanh: a few
 // fp32 ulp of 1; erf: <= 1.5e-7 absolute, Abramowitz & Stegun 7.1.26) is far below the bf16
 // operand rounding of that mode.  The fp32 parity mode uses the libm tanhf / erff / expf.

@@ -33,6 +33,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <type_traits>
 
 #include "../../include/miner_news.h"
 #include "cdna4_common.h"
@@ -447,7 +448,7 @@ template <class T, int CW = 64> struct NCfg {   // CW: columns per chunk (64, or
   static constexpr int RB = CW * (int)sizeof(T);     // bytes of one row of a chunk
   static constexpr int PART = 64 * RB;               // 64 rows: E[his] | proj[his] | Cand
   static constexpr int SLOT = 3 * PART;
-  static constexpr int NSLOT = (sizeof(T) == 2 && CW == 64) ? 4 : 2;
+  static constexpr int NSLOT = RB == 128 ? 4 : 2;      // 128-byte chunk rows: 4 slots of 24 KiB
   static constexpr int NI = RB / 128;                // DMA instructions per part per wave
   static constexpr int RPI = 1024 / RB;              // rows per DMA instruction
   static constexpr int PPR = RB / 16;                // 16-byte pieces per row
@@ -470,7 +471,8 @@ constexpr int kOffSoft = kOffPrep + 2 * kPrepB;      // cooperative softmax part
 constexpr int kNewsLds = kOffSoft + kWaves * 32 * 2 * 4;
 static_assert(kNewsLds <= kLdsMax, "news_score LDS");
 static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>::NSLOT * NCfg<float>::SLOT == kRingB &&
-              NCfg<__bf16, 128>::NSLOT * NCfg<__bf16, 128>::SLOT == kRingB, "ring");
+              NCfg<__bf16, 128>::NSLOT * NCfg<__bf16, 128>::SLOT == kRingB &&
+              NCfg<float, 32>::NSLOT * NCfg<float, 32>::SLOT == kRingB, "ring");
 
 // chunk swizzle of a slot row: bf16 (8 chunks per row, 2 rows per 256-byte bank row): rows 4q..4q+3
 // of a transposed read hit disjoint banks and 16 rows of a ds_read_b128 group distinct slots;
@@ -1142,6 +1144,516 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
 }
 
 // ================================================================================================
+// fp32 scoring (the parity mode and the bench headline): news_score32<ST, RAGGED>
+// ================================================================================================
+// The per-impression math of news_score (model.py:113-138, :176-182, :200-216 on the gathered
+// rows) laid out for the fp32 matrix cores: v_mfma_f32_16x16x4_f32 is an exact fp32 fma chain at
+// the fp32 peak (64 FLOP/clk/SIMD, the rate of 32x32x2 but in 16-row tiles), so the history pads
+// only to a multiple of 4 (50 -> 52, not 64) and the candidates to 16 (40 -> 48, not 64).
+//   * the rows stream in 32-column chunks (128-byte row pieces, 8 rows per LDS-DMA instruction)
+//     through a 4-slot ring, two chunks per barrier: one pair is computed while the next lands;
+//     rows past L / past the candidate count are never fetched (the ring starts zeroed; such rows
+//     meet A = 0 or unstored scores);
+//   * wave w = (path P = w >> 2, column tile ct = (w >> 1) & 1, interest tile kt = w & 1), so each
+//     SIMD pairs a mui wave (P = 0) with an X wave (P = 1, carries the GELU). Per chunk:
+//       muiᵀ / Xᵀ [16 cols x 16 interests] = part[his]ᵀ · Aᵀ     ceil(L/4) MFMAs (model.py:182, :212)
+//       M / Lg [16 cands x 16 interests] += Cand · muiᵀ / Xᵀ      4 MFMAs per candidate tile (:127, :213)
+//     the accumulator of the first product is the B operand of the second (D rows = its k steps);
+//   * per pass (<= 64 candidates) the two column-tile waves of each (P, kt) combine their partials
+//     through LDS (one barrier), the final M / Lg go to LDS, and S7 (:128-136, :214) runs on waves
+//     0-3 at the next item's first chunk.
+constexpr int kF32CW = 32;
+// chunk-row swizzle over the 8 16-byte pieces of a 128-byte row: conflict-free ds_read_b128 of the
+// candidate operand (rows 16t + l, pieces 4ct + g) and ds_read_b32 of the history operand (rows
+// 4s + g of a half wave); found by exhaustive search over GF(2)-linear maps of the row bits
+__host__ __device__ inline int f32swz(int row) { return (((row >> 1) & 1) << 1) | (((row ^ (row >> 2)) & 1) << 2); }
+
+__device__ __forceinline__ void vm_wait_n(int n) {      // s_waitcnt vmcnt(n), n wave-uniform in [0, 6]
+  switch (n) {
+    case 6: vm_wait<6>(); break;
+    case 5: vm_wait<5>(); break;
+    case 4: vm_wait<4>(); break;
+    case 3: vm_wait<3>(); break;
+    case 2: vm_wait<2>(); break;
+    case 1: vm_wait<1>(); break;
+    default: vm_wait<0>(); break;
+  }
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+template <int ST, bool RAGGED>
+__global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using T = float;
+  using Cf = NCfg<float, kF32CW>;
+  constexpr int NS = Cf::NSLOT;
+  static_assert(NS == 4, "ring: a pair of chunks computed while the next pair lands");
+  constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
+  constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
+  const int G = gridDim.x;
+  const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
+  const int L = p.L, d = p.d;
+  const int nchunk = d / kF32CW;
+  const bool coop = nchunk >= 6;                             // cooperative softmax one impression ahead
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const char* tabB = static_cast<const char*>(p.table);
+  const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
+  const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
+  const int P = wave >> 2, ct = (wave >> 1) & 1, kt = wave & 1;
+  const int nsteps = (L + 3) >> 2;
+  const bool k_live = 16 * kt < p.K;
+  const bool path_live = P == 0 || WEIGHTED;
+
+  auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
+  auto cands = [&](int i, int& off, int& cnt) {
+    if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
+    if constexpr (RAGGED) {
+      const int* o = l0_off(smem, i & 7);
+      off = __builtin_amdgcn_readfirstlane(o[0]);
+      cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
+    } else {
+      off = imp_b(i) * p.C;
+      cnt = p.C;
+    }
+    cnt = min(max(cnt, 0), kMaxCand);
+  };
+  // ---- aux DMA jobs, as news_score ----
+  auto issue_L0 = [&](int i) {
+    if (RAGGED && wave == 0 && i < n_i && (threadIdx.x & 63) < 2)
+      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kOffL0 + (i & 7) * kL0B);
+  };
+  auto issue_L1 = [&](int i) {
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const size_t base = (size_t)imp_b(i) * L + min(lane, L - 1);
+    const unsigned l1 = sbase + kOffL1 + (i & 3) * kL1B;
+    if (wave == 1) {
+      dma_b32(p.his_ids + base, l1);
+    } else if (wave == 2) {
+      const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
+      dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
+    } else if (wave == 3) {
+      if (p.bias) dma_b32(p.bias + base, l1 + 512);
+    } else if (WITH_CAND && wave >= 4) {
+      int off, cnt;
+      cands(i, off, cnt);
+      for (int j = wave - 4; j >= 0 && 64 * j < cnt; j += 4) {
+        const int c = min(64 * j + lane, cnt - 1);
+        dma_b32(p.cand_ids + off + c, l1 + 768 + 256 * j);
+      }
+    }
+  };
+  auto issue_L2 = [&](int i) {
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int row = min(8 * wave + (lane >> 3), L - 1);
+    const int piece = min(lane & 7, (p.K >> 2) - 1);
+    const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
+    dma_b128_c(p.logits + (size_t)id * p.K + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+  };
+  auto prep_softmax = [&](int i) {
+    if (wave != 3 || i >= n_i) return;
+    const int l = threadIdx.x & 63;
+    const uint32_t mw = l1_mask(smem, i & 3)[l];
+    const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + l) & 3);
+    const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
+    float mul = 0.f, add = -INFINITY;
+    if (l < L) {
+      mul = keep ? 1.f : 0.f;
+      add = keep ? (p.bias ? l1_bias(smem, i & 3)[l] : 0.f) : 1e-30f;
+    }
+    float* pr = reinterpret_cast<float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    pr[l] = mul;
+    pr[64 + l] = add;
+  };
+  auto soft_phase = [&](int i, int phase) {
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int k = lane & 31, h = lane >> 5;
+    char* lg = smem + kOffLog + (i & 1) * kLogB;
+    const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    float* part = reinterpret_cast<float*>(smem + kOffSoft);
+    const int l0 = 8 * wave + 4 * h;
+    const float4 mu = *reinterpret_cast<const float4*>(pr + l0);
+    const float4 ad = *reinterpret_cast<const float4*>(pr + 64 + l0);
+    const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
+    float x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = __builtin_fmaf(reinterpret_cast<const float*>(lg + (l0 + j) * 128)[k], m4[j], a4[j]);
+    if (phase == 1) {
+      float m = fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3]));
+      float s = 0.f;
+      if (m != -INFINITY) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += expf(x[j] - m);
+      }
+      const float mo = both_max(m);
+      const float so = (m == -INFINITY ? 0.f : s * expf(m - mo));
+      const float st = mo == -INFINITY ? 0.f : both_sum(so);
+      if (h == 0) {
+        part[(wave * 32 + k) * 2] = mo;
+        part[(wave * 32 + k) * 2 + 1] = st;
+      }
+    } else {
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) M = fmaxf(M, part[(w * 32 + k) * 2]);
+      float S = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const float mw = part[(w * 32 + k) * 2];
+        if (mw != -INFINITY) S += part[(w * 32 + k) * 2 + 1] * expf(mw - M);
+      }
+      float inv = 1.0f / S;
+      if (k >= p.K) inv = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) reinterpret_cast<float*>(lg + (l0 + j) * 128)[k] = expf(x[j] - M) * inv;
+    }
+  };
+  // this lane's row offsets for item (i, pass): wave w DMAs rows 8w .. 8w+7 of each part; bit 0 of
+  // lv: history rows live (E, and proj when weighted), bit 1: candidate rows live
+  auto item_offsets = [&](int i, int pass, uint32_t& oH, uint32_t& oC, unsigned& lv) {
+    const int lane = threadIdx.x & 63;
+    const bool live = i < n_i;
+    int off = 0, cnt = 1;
+    if (live) cands(i, off, cnt);
+    const int cntp = max(1, min(64, cnt - 64 * pass));
+    const int row0 = 8 * wave;
+    lv = 0;
+    if (live && row0 < L) lv |= 1u;
+    if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 2u;
+    lv = __builtin_amdgcn_readfirstlane(lv);
+    const int rowp = row0 + (lane >> 3);
+    const uint32_t poff = (uint32_t)(((lane & 7) ^ f32swz(rowp)) << 4);
+    int h = 0, c = 0;
+    if (live) {
+      h = l1_his(smem, i & 3)[min(rowp, L - 1)];
+      if (WITH_CAND) c = l1_cand(smem, i & 3)[min(64 * pass + min(rowp, cntp - 1), kMaxCand - 1)];
+    }
+    h = min(max(h, 0), p.n_news - 1);
+    c = min(max(c, 0), p.n_news - 1);
+    const uint32_t rowBytes = (uint32_t)d * 4u;
+    oH = (uint32_t)h * rowBytes + poff;
+    oC = (uint32_t)c * rowBytes + poff;
+  };
+  const bool abl_nodma = (p.abl & 2) != 0, abl_nocomp = (p.abl & 4) != 0;   // timing ablations (outputs wrong)
+  auto dma32 = [&](uint32_t oH, uint32_t oC, unsigned lv, int ich, int slot) {
+    if (abl_nodma) return;
+    const unsigned m = sbase + slot * Cf::SLOT + wave * 1024;
+    const char* bE = tabB + ich * kF32CW * 4;
+    if (lv & 1u) {
+      dma_row(oH, bE, m);
+      if constexpr (WEIGHTED) dma_row(oH, prjB + ich * kF32CW * 4, m + Cf::PART);
+    }
+    if (lv & 2u) dma_row(oC, bE, m + 2 * Cf::PART);
+  };
+
+  // ---- per-lane LDS offsets (fixed for the launch) ----
+  uint32_t hOff[2], cOff;
+  {
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {       // history operand rows 4s + g, s of parity sp
+      const int row = 4 * sp + g;
+      hOff[sp] = row * 128 + (((4 * ct + (j >> 2)) ^ f32swz(row)) << 4) + (j & 3) * 4;
+    }
+    cOff = j * 128 + (((4 * ct + g) ^ f32swz(j)) << 4);
+  }
+  float aw[16];                                  // Aᵀ B operand: A[16 kt + j][4 s + g]
+  auto load_aw = [&](int i) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const float* lg = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) aw[s] = lg[(4 * s + g) * 32 + 16 * kt + j];
+  };
+  auto softmax_inwave = [&](int i) {       // small d: every wave computes its A slice itself
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const int k = 16 * kt + j;
+    const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
+    const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int l = 4 * s + g;
+      aw[s] = __builtin_fmaf(lgb[l * 32 + k], pr[l], pr[64 + l]);
+      mx = fmaxf(mx, aw[s]);
+    }
+    mx = rows4_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      aw[s] = expf(aw[s] - mx);            // exp(-inf) = 0 past L
+      sum += aw[s];
+    }
+    sum = rows4_sum(sum);
+    float inv = 1.0f / sum;
+    if (k >= p.K) inv = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) aw[s] *= inv;
+  };
+
+  if constexpr (true) {                    // ring rows no DMA writes read as zeros
+    for (int o = (int)threadIdx.x * 16; o < kRingB; o += kThreads * 16)
+      *reinterpret_cast<u32x4*>(smem + o) = u32x4{0u, 0u, 0u, 0u};
+  }
+  // ---- prologue: aux for the first impressions, A of impression 0, then the first pair ----
+  for (int i = 0; i < 4; ++i) issue_L0(i);
+  vm_wait_all();
+  raw_barrier();
+  issue_L1(0); issue_L1(1); issue_L1(2);
+  vm_wait_all();
+  raw_barrier();
+  issue_L2(0); issue_L2(1);
+  prep_softmax(0); prep_softmax(1);
+  vm_wait_all();
+  raw_barrier();
+  if (coop) {
+    soft_phase(0, 1);
+    raw_barrier();
+    soft_phase(0, 2);
+    raw_barrier();
+  }
+  uint32_t cH, cC, nH = 0, nC = 0;
+  unsigned cLv = 0, nLv = 0;
+  item_offsets(0, 0, cH, cC, cLv);
+  dma32(cH, cC, cLv, 0, 0);
+  dma32(cH, cC, cLv, 1, 1);
+
+  f32x4v acc[4];                               // M / Lg partials of this wave, candidate tiles 0..3
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  int pend_off = -1, pend_cnt = 0;
+  int t = 0;
+
+  // S7 on waves 0-3: wave w candidates [16w, 16w+16) of the finished pass, lane (kq, c) interests
+  // [8kq, 8kq+8); the 4 lane rows combined by permlanes (model.py:128-136, :213-214)
+  auto s7 = [&]() {
+    if (wave >= 4) return;
+    const int lane = threadIdx.x & 63;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int c = 16 * wave + cl;
+    const float* F0 = reinterpret_cast<const float*>(smem + kOffX + 16384);
+    const float* F1 = F0 + 2048;
+    const int sw = (c >> 1) & 31;
+    float lg[8], m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = c * 32 + ((8 * kq + j) ^ sw);
+      m[j] = F0[o];
+      if constexpr (WEIGHTED) lg[j] = F1[o];
+    }
+    float sc;
+    if constexpr (WEIGHTED) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, lg[j]);
+      mx = rows4_max(mx);
+      float sm = 0.f, num = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (8 * kq + j < p.K) {
+          const float pe = expf(lg[j] - mx);
+          sm += pe;
+          num = __builtin_fmaf(pe, m[j], num);
+        }
+      }
+      sm = rows4_sum(sm);
+      num = rows4_sum(num);
+      sc = num / sm;
+    } else {
+      if (p.score_type == MINER_SCORE_MAX) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, m[j]);
+        sc = rows4_max(mx);
+      } else {
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) sm += m[j];
+        sc = rows4_sum(sm) / (float)p.K;
+      }
+    }
+    if (kq == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
+  };
+
+
+  // the history and candidate products of the chunk PAIR (cc0, cc0 + 1) in slots t, t + 1; mode: 1
+  // history product, 2 candidate product, 4 mui out. NST history steps (rows 4s + g, s < NST: A = 0
+  // past L) and NT candidate tiles are compile-time, so all LDS reads issue before the MFMAs, and the
+  // two chunks' chains interleave (one chunk's GELU beside the other's MFMAs).
+  auto compute_t = [&](int ci, int cc0, int mode, auto nst_c, auto nt_c) {
+    constexpr int NST = decltype(nst_c)::value;
+    constexpr int NT = decltype(nt_c)::value;
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const char* s0 = smem + (t & (NS - 1)) * Cf::SLOT;
+    const char* s1 = smem + ((t + 1) & (NS - 1)) * Cf::SLOT;
+    float a0[NST], a1[NST];
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {
+      a0[s] = *reinterpret_cast<const float*>(s0 + P * Cf::PART + hOff[s & 1] + (s >> 1) * 1024);
+      a1[s] = *reinterpret_cast<const float*>(s1 + P * Cf::PART + hOff[s & 1] + (s >> 1) * 1024);
+    }
+    f32x4v h00 = f32x4v{0.f, 0.f, 0.f, 0.f}, h01 = h00, h10 = h00, h11 = h00;
+    if (p.abl & 32) { h00[0] = a0[0]; h10[0] = a1[0]; } else
+#pragma unroll
+    for (int s = 0; s < NST; s += 2) {
+      h00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], aw[s], h00, 0, 0, 0);
+      h10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], aw[s], h10, 0, 0, 0);
+      if (s + 1 < NST) {
+        h01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s + 1], aw[s + 1], h01, 0, 0, 0);
+        h11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s + 1], aw[s + 1], h11, 0, 0, 0);
+      }
+    }
+    f32x4v x0 = h00 + h01, x1 = h10 + h11;
+    if ((mode & 4) && 16 * kt + j < p.K) {
+      float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + 16 * kt + j) * d + kF32CW * cc0 + 16 * ct + 4 * g;
+      *reinterpret_cast<float4*>(dst) = make_float4(x0[0], x0[1], x0[2], x0[3]);
+      *reinterpret_cast<float4*>(dst + kF32CW) = make_float4(x1[0], x1[1], x1[2], x1[3]);
+    }
+    if (mode & 2) {
+      f32x4v cf0[NT], cf1[NT];
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        cf0[q] = *reinterpret_cast<const f32x4v*>(s0 + 2 * Cf::PART + cOff + q * 2048);
+        cf1[q] = *reinterpret_cast<const f32x4v*>(s1 + 2 * Cf::PART + cOff + q * 2048);
+      }
+      if (WEIGHTED && P == 1 && !(p.abl & 8)) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x0[e] = gelu_erfc_nr(x0[e]);
+      }
+      if (p.abl & 16) {
+#pragma unroll
+        for (int q = 0; q < NT; ++q) acc[q] += cf0[q] * x0 + cf1[q] * x1;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(cf0[q][e], x0[e], acc[q], 0, 0, 0);
+        }
+        if (WEIGHTED && P == 1 && !(p.abl & 8)) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x1[e] = gelu_erfc_nr(x1[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(cf1[q][e], x1[e], acc[q], 0, 0, 0);
+        }
+      }
+    }
+  };
+  using I4 = std::integral_constant<int, 4>;
+  auto compute = [&](int ci, int cc0, int mode, int ntile) {
+    if (!(mode & 1) || abl_nocomp) return;
+    auto by_nt = [&](auto nst_c) {
+      if (!(mode & 2) || ntile >= 4) compute_t(ci, cc0, mode, nst_c, I4{});
+      else if (ntile == 3) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 3>{});
+      else if (ntile == 2) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 2>{});
+      else compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 1>{});
+    };
+    if (nsteps <= 8) by_nt(std::integral_constant<int, 8>{});
+    else if (nsteps <= 13) by_nt(std::integral_constant<int, 13>{});
+    else by_nt(std::integral_constant<int, 16>{});
+  };
+
+  // static priority for the X-path waves 4-7 (the GELU chain, the longer one of each SIMD's pair)
+  if (!(p.abl & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  const int npair = nchunk >> 1;
+  for (int ci = 0; ci < n_i; ++ci) {
+    int c_off, c_cnt;
+    cands(ci, c_off, c_cnt);
+    const int cn = max(1, (c_cnt + 63) >> 6);
+    for (int cp = 0; cp < cn; ++cp) {
+      const int cntp = min(64, c_cnt - 64 * cp);
+      const int ntile = (max(cntp, 1) + 15) >> 4;
+      const bool need_mui = P == 0 && p.mui_out != nullptr && cp == 0;
+      const bool need_c = WITH_CAND && path_live;
+      const int mode = (k_live && path_live && (need_c || need_mui)) ? (1 | (need_c ? 2 : 0) | (need_mui ? 4 : 0)) : 0;
+      const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
+      for (int u = 0; u < npair; ++u, t += 2) {
+        vm_wait_all();                 // this pair's rows (and every older DMA) landed for this wave,
+        raw_barrier();                 // then for every wave; the previous pair's slots are free
+        if (u == 0) {
+          if (WITH_CAND && pend_off >= 0) s7();
+          pend_off = -1;
+          if (cp == 0) {
+            if (coop) {
+              load_aw(ci);
+            } else {
+              softmax_inwave(ci);
+              raw_barrier();           // every wave has read impression ci's logit rows
+              issue_L2(ci + 2);
+            }
+            issue_L0(ci + 4);
+            issue_L1(ci + 3);
+            prep_softmax(ci + 2);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        } else if (coop && cp == 0) {
+          if (u == 1) {
+            issue_L2(ci + 2);          // into the rows A of ci was read from (free since the barrier)
+            soft_phase(ci + 1, 1);
+          } else if (u == 2) {
+            soft_phase(ci + 1, 2);
+          }
+        }
+        if (u + 1 < npair) {           // the next pair of this item, else the first pair of the next one
+          dma32(cH, cC, cLv, 2 * u + 2, (t + 2) & (NS - 1));
+          dma32(cH, cC, cLv, 2 * u + 3, (t + 3) & (NS - 1));
+        } else {
+          item_offsets(ni, np, nH, nC, nLv);
+          dma32(nH, nC, nLv, 0, (t + 2) & (NS - 1));
+          dma32(nH, nC, nLv, 1, (t + 3) & (NS - 1));
+        }
+        compute(ci, 2 * u, mode, ntile);
+      }
+      if constexpr (WITH_CAND) {
+        // pass done: the ct = 1 waves hand their partials to the ct = 0 waves of the same (P, kt),
+        // which publish the final M / Lg [c][k ^ swizzle] for S7
+        const int lane = threadIdx.x & 63;
+        const int j = lane & 15, g = lane >> 4;
+        float* R = reinterpret_cast<float*>(smem + kOffX) + (P * 2 + kt) * 1024;
+        if (path_live && k_live && ct == 1) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (q < ntile) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) R[(16 * q + 4 * g + e) * 16 + j] = acc[q][e];
+            }
+          }
+        }
+        raw_barrier();
+        if (path_live && k_live && ct == 0) {
+          float* F = reinterpret_cast<float*>(smem + kOffX + 16384) + P * 2048;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (q < ntile) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int c = 16 * q + 4 * g + e;
+                F[c * 32 + ((16 * kt + j) ^ ((c >> 1) & 31))] = acc[q][e] + R[c * 16 + j];
+              }
+            }
+          }
+        }
+      }
+      pend_off = c_off + 64 * cp;
+      pend_cnt = cntp;
+      cH = nH; cC = nC; cLv = nLv;
+    }
+  }
+  vm_wait_all();
+  raw_barrier();
+  if (WITH_CAND && pend_off >= 0) s7();
+}
+
+// ================================================================================================
 // host side
 // ================================================================================================
 int num_cus() {
@@ -1229,6 +1741,13 @@ int launch_score(void* stream, const NsParams& prm) {
       NEWS_PICK(2, 64)
     } else {
       NEWS_PICK(1, 64)
+    }
+  } else if (!getenv("MINER_NEWS_F32V1")) {
+    // fp32: news_score32 (16x16x4 fp32 MFMA tiles, 32-column chunks computed in pairs)
+    switch (prm.score_type) {
+      case MINER_SCORE_WEIGHTED: kern = rg ? news_score32<MINER_SCORE_WEIGHTED, true> : news_score32<MINER_SCORE_WEIGHTED, false>; break;
+      case MINER_SCORE_NONE: kern = news_score32<MINER_SCORE_NONE, false>; break;
+      default: kern = rg ? news_score32<MINER_SCORE_MAX, true> : news_score32<MINER_SCORE_MAX, false>; break;
     }
   } else {
     NEWS_PICK(1, 64)

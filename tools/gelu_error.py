@@ -1,0 +1,38 @@
+"""Error of the fp32 GELU of the parity kernels (cdna4_common.h gelu_erfc_nr) against float64,
+emulated in float32 numpy (the device's v_rcp_f32 / v_exp_f32 add about 1 ulp each).
+
+    python tools/gelu_error.py      -> max |Δ| / max(1, |x|) over [-10, 10] and log grids
+"""
+from math import erfc, sqrt
+
+import numpy as np
+
+f32 = np.float32
+C = [0.17087277, -0.82215223, 1.48851587, -1.13520398, 0.27886807, -0.18628806, 0.09678418, 0.37409196,
+     1.00002368, -1.26551223]
+
+
+def gelu_nr(x):
+    x = f32(x)
+    z = f32(abs(x) * f32(0.70710678118654752440))
+    t = f32(1) / f32(f32(1) + f32(0.5) * z)
+    q = f32(C[0])
+    for k in C[1:]:
+        q = f32(f32(q * t) + f32(k))
+    y = f32(f32(-z * z) + q)
+    ec = f32(t * f32(np.exp2(f32(y * f32(1.4426950408889634)))))
+    phi = f32(0.5) * ec if x < 0 else f32(1) - f32(0.5) * ec
+    return f32(x * phi)
+
+
+def max_error():
+    xs = np.concatenate([np.linspace(-10, 10, 200001), np.logspace(-8, 1, 2000), -np.logspace(-8, 1, 2000)])
+    worst = 0.0
+    for x in xs:
+        ref = 0.5 * x * erfc(-x / sqrt(2))
+        worst = max(worst, abs(float(gelu_nr(x)) - ref) / max(1.0, abs(x)))
+    return worst
+
+
+if __name__ == "__main__":
+    print(f"max |gelu_nr - gelu| / max(1, |x|) = {max_error():.3e}")

@@ -1,0 +1,30 @@
+"""Run the news-path scoring kernel `reps` times at config-3 shape (for rocprofv3 passes).
+
+    python tools/news_once.py [fp32|bf16] [B] [reps]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from miner_amd import news, ops, synthetic  # noqa: E402
+
+dev = "cuda:0"
+dt = torch.float32 if (len(sys.argv) < 2 or sys.argv[1] == "fp32") else torch.bfloat16
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 131072
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+n_news, L, C, d, K, Dc = 104000, 50, 40, 768, 32, 200
+g = torch.Generator(device=dev).manual_seed(36)
+table = (torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5).to(dt)
+lens = torch.randint(0, L + 1, (B,), generator=g, device=dev)
+mask = torch.arange(L, device=dev)[None, :] >= (L - lens)[:, None]
+hid = torch.randint(1, n_news, (B, L), generator=g, device=dev, dtype=torch.int32)
+hid[~mask] = 0
+cid = torch.randint(1, n_news, (B, C), generator=g, device=dev, dtype=torch.int32)
+W1, Q, W2 = synthetic.init_weights(36, d, Dc, K, device=dev)
+nt = news.precompute(table, ops.pack_weights(W1, Q, W2, dtype=dt))
+for _ in range(reps):
+    s = news.score(nt, hid, mask, cid, validate=False)
+torch.cuda.synchronize()
+print("ok", float(s.float().abs().mean()))
