@@ -254,12 +254,12 @@ def load_pmc(path, workload, B):
 
 def measure_news(table, W1, Q, W2, pool, steps, warmup, world, dev):
     """One dtype of the news path: per step precompute + score over pool[i % len(pool)].
-    Returns (elapsed s, precompute ms, scoring ms, last scores, NewsTable)."""
+    Returns (elapsed s, precompute ms, scoring ms, {pool index: scores of its last step}, NewsTable)."""
     from miner_amd import news, ops
     pw = ops.pack_weights(W1, Q, W2, dtype=table.dtype)      # once per model, outside the timed region
     nt = news.precompute(table, pw)
     tm = EventTimer(dev, 2)
-    out = [None]
+    out = {}
 
     def step(i, timed):
         nonlocal nt
@@ -270,12 +270,12 @@ def measure_news(table, W1, Q, W2, pool, steps, warmup, world, dev):
         nt = news.precompute(table, pw, out=nt)
         if e:
             e[1].record(tm.stream)
-        out[0] = news.score(nt, hid, mask, cid, validate=False)
+        out[i % len(pool)] = news.score(nt, hid, mask, cid, validate=False)
         if e:
             e[2].record(tm.stream)
 
     elapsed = timed_steps(step, steps, warmup, world, dev)
-    return elapsed, tm.mean_ms(0), tm.mean_ms(1), out[0], nt
+    return elapsed, tm.mean_ms(0), tm.mean_ms(1), out, nt
 
 
 def roofline_news(B, kern_ms, elem, d=D, pmc=None, kernel=""):
@@ -326,19 +326,20 @@ def device_metrics(scores, dev):
     return lab, offs, m, (time.perf_counter() - t0) * 1e3
 
 
-def auc_parity(nt16, nt32, batch, table32, W1, Q, W2, dev, n_imp=2048):
+def auc_parity(s32_full, s16_full, batch, table32, W1, Q, W2, dev, n_imp=2048):
     """The metric's "AUC parity vs ref", on a bounded sample of the timed batch (part of the CPU
     baseline leg): scores of the reference CPU path (the oracle: model.py:113-216 as the same torch
     fp32 ops on the host) vs the GPU news path in fp32 (the headline mode) and in bf16, then the
     reference's metrics (evaluation.py:36-84, via the GPU metrics kernels) over one set of labels:
     Bernoulli(sigmoid(2·z)) of the reference's z-scored scores, with >= 1 click and >= 1 non-click per
-    impression (reader.py:374)."""
+    impression (reader.py:374). The GPU scores are the first n_imp rows of the timed steps' own output
+    for this batch (impressions are independent), so this leg launches no scoring kernel and the
+    rocprof average of the headline kernel is over the timed launches only."""
     try:
-        from miner_amd import metrics, news
+        from miner_amd import metrics
         from oracle import miner_oracle as orc
         hid, mask, cid = [x[:n_imp] for x in batch]
-        s32 = news.score(nt32, hid, mask, cid, validate=False)
-        s16 = news.score(nt16, hid, mask, cid, validate=False)
+        s32, s16 = s32_full[:n_imp], s16_full[:n_imp]
         T = table32.cpu()
         h, c = hid.cpu().long(), cid.cpu().long()
         with torch.no_grad():
@@ -406,11 +407,13 @@ def run_news(args, rank, world, dev):
     torch.cuda.synchronize()
 
     # headline: fp32 (the reference's precision)
-    el32, pre32, kern32, s32, nt32 = measure_news(table32, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+    el32, pre32, kern32, o32, nt32 = measure_news(table32, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+    s32 = o32[0]
     assert torch.isfinite(s32).all()
     # bf16 throughput mode, same batch and protocol
     table16 = table32.to(torch.bfloat16)
-    el16, pre16, kern16, s16, nt16 = measure_news(table16, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+    el16, pre16, kern16, o16, nt16 = measure_news(table16, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+    s16 = o16[0]
     assert torch.isfinite(s16).all()
     c2 = config2_line(args, rank, world, dev) if not args.no_config2 else None
     dense = dense_kernel_line(dev) if (world == 1 and not args.no_dense) else None
@@ -420,7 +423,7 @@ def run_news(args, rank, world, dev):
     value = B * C * args.steps * world / el32
     pmc32 = load_pmc(args.news_traffic32, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_fp32", B)
     pmc16 = load_pmc(args.news_traffic, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_bf16", B)
-    roof = roofline_news(B, kern32, 4, pmc=pmc32, kernel="news_score<fp32,weighted>")
+    roof = roofline_news(B, kern32, 4, pmc=pmc32, kernel="news_score32<weighted, dense, fp32 MFMA, 24 chunks>")
     pre_fl = news_precompute_flops(N_NEWS, D, DC, K)
     # metric step on the device over the whole fp32 batch, and the bf16 AUC delta at full size
     metric_step = None
@@ -441,7 +444,7 @@ def run_news(args, rank, world, dev):
                  "note": "bf16 operands, fp32 accumulation: no reference counterpart (the reference evaluates "
                          "in fp32); its metric deltas vs the fp32 headline are in metric_step.bf16_delta"}
     cpu = cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
-    auc = auc_parity(nt16, nt32, pool[0], table32, W1, Q, W2, dev) if (world == 1 and not args.no_cpu) else None
+    auc = auc_parity(s32, s16, pool[0], table32, W1, Q, W2, dev) if (world == 1 and not args.no_cpu) else None
     line = {
         "metric": METRIC,
         "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
@@ -672,7 +675,7 @@ def run_corpus(args, rank, world, dev):
         mask = torch.arange(C5_L, device=dev)[None, :] >= (C5_L - lens)[:, None]
         pool.append((hid, mask))
     tm = EventTimer(dev, 2)
-    out = [None]
+    out = {}
 
     def step(i, timed):
         hid, mask = pool[i % len(pool)]

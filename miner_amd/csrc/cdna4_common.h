@@ -180,6 +180,57 @@ __device__ __forceinline__ float gelu_erfc_nr(float x) {
   return x * phi;
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 contractions on the bf16 matrix cores (bf16x6): an fp32 value is cut into three bf16 terms
+// by truncation, x = hi + mid + lo EXACTLY (hi takes the top 8 significand bits, mid the top 8 of
+// the exact remainder x - hi, and the remainder after that has at most 8 significant bits, so lo
+// holds it exactly). A product a·b is then the six partial products whose order is at most 2^-16
+// (al·bh, ah·bl, am·bm, am·bh, ah·bm, ah·bh — every product of two bf16 values is exact in fp32);
+// what is dropped (am·bl, al·bm, al·bl) is below 2^-23·|a·b|, under the rounding of the fp32 sum.
+// Six v_mfma_f32_16x16x32_bf16 (16 cycles each) replace the fp32 MFMA work of one contraction at
+// 1/16 of the bf16 rate: 2.67x the fp32 rate, and unlike the fp32 MFMA they co-issue with VALU.
+// ---------------------------------------------------------------------------------------------
+struct Split8 { u32x4 hi, mid, lo; };       // 8 fp32 elements as three bf16x8 operands
+
+__device__ __forceinline__ unsigned hi16_pack(unsigned a, unsigned b) {   // (a >> 16) | (b & 0xffff0000)
+  return __builtin_amdgcn_perm(b, a, 0x07060302u);
+}
+__device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+  const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+  hi = hi16_pack(u0, u1);
+  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+  const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+  mid = hi16_pack(v0, v1);
+  const float q0 = r0 - __uint_as_float(v0 & 0xffff0000u), q1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+  lo = hi16_pack(__float_as_uint(q0), __float_as_uint(q1));
+}
+__device__ __forceinline__ Split8 split8(const float* x) {
+  Split8 s;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    unsigned h, md, l;
+    split3_pair(x[2 * m], x[2 * m + 1], h, md, l);
+    s.hi[m] = h;
+    s.mid[m] = md;
+    s.lo[m] = l;
+  }
+  return s;
+}
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// c += A·B over 32 contraction indices at fp32 accuracy; A-operand lane map A[row l&15][k 8(l>>4)+e],
+// B-operand B[k 8(l>>4)+e][col l&15], smallest terms first
+__device__ __forceinline__ f32x4 mma_x6(f32x4 c, const Split8& a, const Split8& b) {
+  c = mfma16_bf16(a.lo, b.hi, c);
+  c = mfma16_bf16(a.hi, b.lo, c);
+  c = mfma16_bf16(a.mid, b.mid, c);
+  c = mfma16_bf16(a.mid, b.hi, c);
+  c = mfma16_bf16(a.hi, b.mid, c);
+  return mfma16_bf16(a.hi, b.hi, c);
+}
+
 // bf16-mode transcendentals: branch-free, a handful of VALU ops each.  Their error (tanh: a few
 // fp32 ulp of 1; erf: <= 1.5e-7 absolute, Abramowitz & Stegun 7.1.26) is far below the bf16
 // operand rounding of that mode.  The fp32 parity mode uses the libm tanhf / erff / expf.

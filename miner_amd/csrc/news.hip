@@ -444,6 +444,20 @@ __device__ __forceinline__ bool dbg_ok(int kind, const void* a, size_t n, const 
 #define NEWS_CHK(kind, a, n, lo, range, lds, lds_n)
 #endif
 
+// diagnostic build only (-DMINER_STAMPS): per-wave stage cycles of news_score32 (lane 0 of each wave
+// sums s_memtime deltas; read with miner_news_debug_stage_cycles)
+#ifdef MINER_STAMPS
+__device__ unsigned long long g_ns_stage[kWaves][8];
+__device__ unsigned long long g_ns_items;
+#define NS_STAMP_DECL unsigned long long st_acc[8] = {0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define NS_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } while (0)
+#define NS_STAMP_FLUSH(n) do { if ((threadIdx.x & 63) == 0) { for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_ns_stage[threadIdx.x >> 6][i_], st_acc[i_]); if (threadIdx.x == 0) atomicAdd(&g_ns_items, (unsigned long long)(n)); } } while (0)
+#else
+#define NS_STAMP_DECL
+#define NS_STAMP(i) do {} while (0)
+#define NS_STAMP_FLUSH(n) do {} while (0)
+#endif
+
 template <class T, int CW = 64> struct NCfg {   // CW: columns per chunk (64, or 128 for 16-bit)
   static constexpr int RB = CW * (int)sizeof(T);     // bytes of one row of a chunk
   static constexpr int PART = 64 * RB;               // 64 rows: E[his] | proj[his] | Cand
@@ -1162,11 +1176,34 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
 //   * per pass (<= 64 candidates) the two column-tile waves of each (P, kt) combine their partials
 //     through LDS (one barrier), the final M / Lg go to LDS, and S7 (:128-136, :214) runs on waves
 //     0-3 at the next item's first chunk.
+// X6 = true (MINER_NEWS_F32X6=1): the same stream and the same products on the bf16 matrix cores
+// at fp32 accuracy (bf16x6, cdna4_common.h: every fp32 operand cut exactly into three bf16 terms,
+// six v_mfma_f32_16x16x32_bf16 per 32-index contraction). Wave w = (P, chunk cc = (w >> 1) & 1 of the
+// pair, kt); per pair each wave takes ONE whole 32-column chunk:
+//       muiᵀ / Xᵀ [32 cols x 16 interests] = part[his]ᵀ · Aᵀ   2 column tiles (even / odd columns,
+//           one ds_read_b64 per row) x ceil(L/32) x 6 MFMAs; history padded to 32 / 64
+//       M / Lg [16 cands x 16 interests] += Cand · muiᵀ / Xᵀ    6 MFMAs per candidate tile
+//     the two accumulators of the first product are the B operand of the second as they stand:
+//     lane (j, g) holds columns 2(4g + e) and 2(4g + e) + 1 = the contraction indices 8g .. 8g + 7.
+//     The fp32 MFMA cannot co-issue with VALU; the bf16 MFMA does, so one SIMD's GELU / split VALU
+//     work runs beside the other wave's MFMAs. Measured (tools/news_stages.py): equal to the fp32
+//     MFMA form at config 3 (15.5 vs 15.6 ms per 131k): the MFMA time saved (1344 vs 3200 cycles
+//     per pair per SIMD) goes to the split VALU (2x redundant for the history rows, 4x for the
+//     candidate rows across the waves), and both share ~2.3k cycles per pair of DMA issue, softmax,
+//     S7 and pass-end work.
 constexpr int kF32CW = 32;
 // chunk-row swizzle over the 8 16-byte pieces of a 128-byte row: conflict-free ds_read_b128 of the
 // candidate operand (rows 16t + l, pieces 4ct + g) and ds_read_b32 of the history operand (rows
 // 4s + g of a half wave); found by exhaustive search over GF(2)-linear maps of the row bits
 __host__ __device__ inline int f32swz(int row) { return (((row >> 1) & 1) << 1) | (((row ^ (row >> 2)) & 1) << 2); }
+// bf16x6 layout of a part: physical row 8b + i holds logical row 8b + (i ^ (b & 1)) (x6row, an
+// involution), and its 16-byte piece slot s holds logical piece s ^ x6swz(physical row). Then the
+// ds_read_b64 of the history operand (lanes g = 0, 1 of a half read logical rows 8g + i, whole
+// 128-byte rows) puts the half's two rows in different 128-byte bank halves, and the ds_read_b128 of
+// the candidate operand (rows 16q + j, pieces 2g + u) is conflict-free in all four lane groups
+// (exhaustive search over GF(2)-linear maps of the physical row bits)
+__host__ __device__ inline int x6row(int row) { return row ^ ((row >> 3) & 1); }
+__host__ __device__ inline int x6swz(int prow) { return ((prow >> 1) & 1) | (prow & 4); }
 
 __device__ __forceinline__ void vm_wait_n(int n) {      // s_waitcnt vmcnt(n), n wave-uniform in [0, 6]
   switch (n) {
@@ -1182,7 +1219,7 @@ __device__ __forceinline__ void vm_wait_n(int n) {      // s_waitcnt vmcnt(n), n
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-template <int ST, bool RAGGED>
+template <int ST, bool RAGGED, bool X6, int NCH>         // NCH: 32-column chunks per row (0: d / 32 at run time)
 __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using T = float;
@@ -1194,13 +1231,13 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int L = p.L, d = p.d;
-  const int nchunk = d / kF32CW;
+  const int nchunk = NCH > 0 ? NCH : d / kF32CW;
   const bool coop = nchunk >= 6;                             // cooperative softmax one impression ahead
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const char* tabB = static_cast<const char*>(p.table);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
-  const int P = wave >> 2, ct = (wave >> 1) & 1, kt = wave & 1;
+  const int P = wave >> 2, ct = (wave >> 1) & 1, kt = wave & 1;   // X6: ct = the chunk of the pair
   const int nsteps = (L + 3) >> 2;
   const bool k_live = 16 * kt < p.K;
   const bool path_live = P == 0 || WEIGHTED;
@@ -1324,8 +1361,9 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     if (live && row0 < L) lv |= 1u;
     if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 2u;
     lv = __builtin_amdgcn_readfirstlane(lv);
-    const int rowp = row0 + (lane >> 3);
-    const uint32_t poff = (uint32_t)(((lane & 7) ^ f32swz(rowp)) << 4);
+    const int prow = row0 + (lane >> 3);                    // the ring row this lane fills
+    const int rowp = X6 ? x6row(prow) : prow;                // the logical row it fetches
+    const uint32_t poff = (uint32_t)(((lane & 7) ^ (X6 ? x6swz(prow) : f32swz(rowp))) << 4);
     int h = 0, c = 0;
     if (live) {
       h = l1_his(smem, i & 3)[min(rowp, L - 1)];
@@ -1338,6 +1376,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     oC = (uint32_t)c * rowBytes + poff;
   };
   const bool abl_nodma = (p.abl & 2) != 0, abl_nocomp = (p.abl & 4) != 0;   // timing ablations (outputs wrong)
+  NS_STAMP_DECL
   auto dma32 = [&](uint32_t oH, uint32_t oC, unsigned lv, int ich, int slot) {
     if (abl_nodma) return;
     const unsigned m = sbase + slot * Cf::SLOT + wave * 1024;
@@ -1361,13 +1400,39 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     }
     cOff = j * 128 + (((4 * ct + g) ^ f32swz(j)) << 4);
   }
-  float aw[16];                                  // Aᵀ B operand: A[16 kt + j][4 s + g]
+  // X6: history operand rows 8g + i of a 32-row block, columns 2j, 2j + 1 (one ds_read_b64; the
+  // block offset 4096 kb is added at the read); candidate operand rows 16q + j, pieces 2g + u
+  uint32_t xeOff[8], xcOff[2];
+  if constexpr (X6) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pr = x6row(8 * g + i);
+      xeOff[i] = pr * 128 + (((j >> 1) ^ x6swz(pr)) << 4) + (j & 1) * 8;
+    }
+    const int prc = x6row(j);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) xcOff[u] = prc * 128 + (((2 * g + u) ^ x6swz(prc)) << 4);
+  }
+  // Aᵀ B operand: aw[s] = A[16 kt + j][aw_row(s)]; fp32 MFMA: history slot 4s + g; X6: slot
+  // 32 (s >> 3) + 8g + (s & 7), split per 32-slot block into awx[kb]
+  float aw[16];
+  Split8 awx[2];
+  auto aw_row = [&](int s, int g) { return X6 ? 32 * (s >> 3) + 8 * g + (s & 7) : 4 * s + g; };
+  auto split_aw = [&]() {
+    if constexpr (X6) {
+      awx[0] = split8(aw);
+      awx[1] = split8(aw + 8);
+    }
+  };
   auto load_aw = [&](int i) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const float* lg = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) aw[s] = lg[(4 * s + g) * 32 + 16 * kt + j];
+    for (int s = 0; s < 16; ++s) aw[s] = lg[aw_row(s, g) * 32 + 16 * kt + j];
+    split_aw();
   };
   auto softmax_inwave = [&](int i) {       // small d: every wave computes its A slice itself
     const int lane = threadIdx.x & 63;
@@ -1378,7 +1443,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     float mx = -INFINITY;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int l = 4 * s + g;
+      const int l = aw_row(s, g);
       aw[s] = __builtin_fmaf(lgb[l * 32 + k], pr[l], pr[64 + l]);
       mx = fmaxf(mx, aw[s]);
     }
@@ -1394,6 +1459,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     if (k >= p.K) inv = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) aw[s] *= inv;
+    split_aw();
   };
 
   if constexpr (true) {                    // ring rows no DMA writes read as zeros
@@ -1547,9 +1613,80 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       }
     }
   };
+  // X6: this wave's chunk cc0 + ct of the pair (slot t + ct); NKB 32-slot history blocks, NT
+  // candidate tiles, compile-time
+  auto compute_x6 = [&](int ci, int cc0, int mode, auto nkb_c, auto nt_c) {
+    constexpr int NKB = decltype(nkb_c)::value;
+    constexpr int NT = decltype(nt_c)::value;
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const char* sl = smem + ((t + ct) & (NS - 1)) * Cf::SLOT;
+    const char* hp = sl + P * Cf::PART;
+    f32x4v h0 = f32x4v{0.f, 0.f, 0.f, 0.f}, h1 = h0;    // columns 2(4g + e) and 2(4g + e) + 1
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      float e0[8], e1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float2 v = *reinterpret_cast<const float2*>(hp + kb * 4096 + xeOff[i]);
+        e0[i] = v.x;
+        e1[i] = v.y;
+      }
+      if (p.abl & 32) {                        // timing ablation: no history product
+        h0[0] += e0[0];
+        h1[0] += e1[0];
+      } else {
+        h0 = mma_x6(h0, split8(e0), awx[kb]);
+        h1 = mma_x6(h1, split8(e1), awx[kb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);       // one block's operands live at a time (VGPR budget)
+    }
+    NS_STAMP(4);
+    const int col0 = kF32CW * (cc0 + ct) + 8 * g;          // this lane's columns col0 .. col0 + 7
+    if ((mode & 4) && 16 * kt + j < p.K) {
+      float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + 16 * kt + j) * d + col0;
+      *reinterpret_cast<float4*>(dst) = make_float4(h0[0], h1[0], h0[1], h1[1]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(h0[2], h1[2], h0[3], h1[3]);
+    }
+    if (mode & 2) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[2 * e] = h0[e];
+        x[2 * e + 1] = h1[e];
+      }
+      if (WEIGHTED && P == 1 && !(p.abl & 8)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = gelu_erfc_nr(x[i]);
+      }
+      const Split8 sb = split8(x);
+      NS_STAMP(5);
+      const char* cpart = sl + 2 * Cf::PART;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        float c[8];
+        *reinterpret_cast<float4*>(c) = *reinterpret_cast<const float4*>(cpart + q * 2048 + xcOff[0]);
+        *reinterpret_cast<float4*>(c + 4) = *reinterpret_cast<const float4*>(cpart + q * 2048 + xcOff[1]);
+        if (p.abl & 16) acc[q][0] += c[0] + sb.hi[0];   // timing ablation: no candidate product
+        else acc[q] = mma_x6(acc[q], split8(c), sb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
   using I4 = std::integral_constant<int, 4>;
   auto compute = [&](int ci, int cc0, int mode, int ntile) {
     if (!(mode & 1) || abl_nocomp) return;
+    if constexpr (X6) {
+      auto by_nt = [&](auto nkb_c) {
+        if (!(mode & 2) || ntile >= 4) compute_x6(ci, cc0, mode, nkb_c, I4{});
+        else if (ntile == 3) compute_x6(ci, cc0, mode, nkb_c, std::integral_constant<int, 3>{});
+        else if (ntile == 2) compute_x6(ci, cc0, mode, nkb_c, std::integral_constant<int, 2>{});
+        else compute_x6(ci, cc0, mode, nkb_c, std::integral_constant<int, 1>{});
+      };
+      if (L <= 32) by_nt(std::integral_constant<int, 1>{});
+      else by_nt(std::integral_constant<int, 2>{});
+      return;
+    }
     auto by_nt = [&](auto nst_c) {
       if (!(mode & 2) || ntile >= 4) compute_t(ci, cc0, mode, nst_c, I4{});
       else if (ntile == 3) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 3>{});
@@ -1576,8 +1713,11 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       const int mode = (k_live && path_live && (need_c || need_mui)) ? (1 | (need_c ? 2 : 0) | (need_mui ? 4 : 0)) : 0;
       const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
       for (int u = 0; u < npair; ++u, t += 2) {
+        NS_STAMP(7);
         vm_wait_all();                 // this pair's rows (and every older DMA) landed for this wave,
+        NS_STAMP(0);
         raw_barrier();                 // then for every wave; the previous pair's slots are free
+        NS_STAMP(1);
         if (u == 0) {
           if (WITH_CAND && pend_off >= 0) s7();
           pend_off = -1;
@@ -1603,6 +1743,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
             soft_phase(ci + 1, 2);
           }
         }
+        NS_STAMP(2);
         if (u + 1 < npair) {           // the next pair of this item, else the first pair of the next one
           dma32(cH, cC, cLv, 2 * u + 2, (t + 2) & (NS - 1));
           dma32(cH, cC, cLv, 2 * u + 3, (t + 3) & (NS - 1));
@@ -1611,7 +1752,9 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           dma32(nH, nC, nLv, 0, (t + 2) & (NS - 1));
           dma32(nH, nC, nLv, 1, (t + 3) & (NS - 1));
         }
+        NS_STAMP(3);
         compute(ci, 2 * u, mode, ntile);
+        NS_STAMP(6);
       }
       if constexpr (WITH_CAND) {
         // pass done: the ct = 1 waves hand their partials to the ct = 0 waves of the same (P, kt),
@@ -1646,8 +1789,10 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       pend_off = c_off + 64 * cp;
       pend_cnt = cntp;
       cH = nH; cC = nC; cLv = nLv;
+      NS_STAMP(7);
     }
   }
+  NS_STAMP_FLUSH(n_i);
   vm_wait_all();
   raw_barrier();
   if (WITH_CAND && pend_off >= 0) s7();
@@ -1744,11 +1889,21 @@ int launch_score(void* stream, const NsParams& prm) {
     }
   } else if (!getenv("MINER_NEWS_F32V1")) {
     // fp32: news_score32 (16x16x4 fp32 MFMA tiles, 32-column chunks computed in pairs)
-    switch (prm.score_type) {
-      case MINER_SCORE_WEIGHTED: kern = rg ? news_score32<MINER_SCORE_WEIGHTED, true> : news_score32<MINER_SCORE_WEIGHTED, false>; break;
-      case MINER_SCORE_NONE: kern = news_score32<MINER_SCORE_NONE, false>; break;
-      default: kern = rg ? news_score32<MINER_SCORE_MAX, true> : news_score32<MINER_SCORE_MAX, false>; break;
+    // fp32: news_score32 on the fp32 matrix cores (exact fp32 fma chains); MINER_NEWS_F32X6=1 selects
+    // the bf16x6 form (same accuracy class, bf16 matrix cores; measured equal speed at config 3)
+#define NEWS_PICK32(X6V, NCH)                                                                            \
+    switch (prm.score_type) {                                                                            \
+      case MINER_SCORE_WEIGHTED: kern = rg ? news_score32<MINER_SCORE_WEIGHTED, true, X6V, NCH> : news_score32<MINER_SCORE_WEIGHTED, false, X6V, NCH>; break; \
+      case MINER_SCORE_NONE: kern = news_score32<MINER_SCORE_NONE, false, X6V, NCH>; break;               \
+      default: kern = rg ? news_score32<MINER_SCORE_MAX, true, X6V, NCH> : news_score32<MINER_SCORE_MAX, false, X6V, NCH>; break; \
     }
+    const bool x6 = getenv("MINER_NEWS_F32X6") != nullptr;
+    if (prm.d == 768) {                // config 3 (MIND-large): the chunk count compile-time
+      if (x6) { NEWS_PICK32(true, 24) } else { NEWS_PICK32(false, 24) }
+    } else {
+      if (x6) { NEWS_PICK32(true, 0) } else { NEWS_PICK32(false, 0) }
+    }
+#undef NEWS_PICK32
   } else {
     NEWS_PICK(1, 64)
   }
@@ -1774,6 +1929,20 @@ int launch_score(void* stream, const NsParams& prm) {
 }  // namespace
 
 extern "C" {
+
+#ifdef MINER_STAMPS
+// diagnostic build only: read (and reset) the per-wave stage cycles of news_score32;
+// out[8 w + i] = cycles of stage i of wave w summed over workgroups, out[64] = impressions
+int miner_news_debug_stage_cycles(unsigned long long* out) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ns_stage), 64 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_ns_items), sizeof(unsigned long long));
+  unsigned long long z[64] = {0};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_ns_stage), z, 64 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_ns_items), z, sizeof(unsigned long long));
+  return (int)e;
+}
+#endif
 
 int miner_news_supported(int dtype, int L, int d, int Dc, int K) {
   const int rc = check_news(dtype, L, d, Dc, K);

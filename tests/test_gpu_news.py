@@ -95,6 +95,38 @@ def test_fp32_matches_reference(name):
     _ok(mui, g["mui"], torch.float32, f"{name} mui")
 
 
+@pytest.mark.parametrize("name", golden_names())
+def test_fp32_bf16x6_matches_reference(name, monkeypatch):
+    """The optional bf16x6 form of the fp32 kernel (MINER_NEWS_F32X6=1: every fp32 operand cut exactly
+    into three bf16 terms, six bf16 MFMAs per contraction) at the same fp32 bar as the default."""
+    monkeypatch.setenv("MINER_NEWS_F32X6", "1")
+    test_fp32_matches_reference(name)
+
+
+@pytest.mark.parametrize("x6", [False, True])
+def test_fp32_config3_vs_f64(x6, monkeypatch):
+    """Config-3 shape (L=50, C=40, K=32, d=768) against a float64 evaluation of the same products:
+    both fp32 forms (fp32 MFMA fma chains, bf16x6) stay well inside the fp32 parity bar."""
+    if x6:
+        monkeypatch.setenv("MINER_NEWS_F32X6", "1")
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(33, 300, 50, 768, 5000, torch.float32)
+    nt = news.precompute(table, W1, Q, W2)
+    scores = news.score(nt, hid, mask, cid)
+    torch.cuda.synchronize()
+    T = table.double().cpu()
+    E, Cd = T[hid.cpu().long()], T[cid.cpu().long()]
+    w1, q, w2 = (x.double().cpu() for x in (W1, Q, W2))
+    s = torch.tanh(E @ w1.T) @ q.T                                       # [B, L, K]
+    s = s.masked_fill(~mask.cpu()[:, :, None], 1e-30)
+    a = torch.softmax(s, dim=1)
+    mui = torch.einsum("blk,bld->bkd", a, E)
+    x = torch.nn.functional.gelu(mui @ w2.T)
+    m = Cd @ mui.transpose(1, 2)
+    lg = torch.softmax(Cd @ x.transpose(1, 2), dim=-1)
+    ref = (lg * m).sum(-1)
+    _ok(scores, ref, torch.float32, f"config-3 fp32 (x6={x6}) vs float64")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("d,Dc,K", [(64, 32, 4), (256, 200, 32), (768, 200, 32), (192, 72, 16)])
 def test_precompute_vs_f64(dtype, d, Dc, K):

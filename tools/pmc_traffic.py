@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--news", action="store_true",
                     help="the news-path scoring kernel news_score<bf16, weighted, dense> (bench.py config3)")
+    ap.add_argument("--news32", action="store_true",
+                    help="the fp32 news-path scoring kernel news_score32<weighted, dense> (the bench headline)")
     args = ap.parse_args()
     workload, kernel = "L50_K32_d768_Dc200_C40_bf16", "miner_fused<bf16,full>"
     if args.news:
@@ -61,6 +63,11 @@ def main():
         workload, kernel = "news_L50_K32_d768_C40_N104000_bf16", "news_score<bf16,weighted>"
         if args.out == os.path.join(ROOT, "profiles", "pmc_traffic.json"):
             args.out = os.path.join(ROOT, "profiles", "pmc_traffic_news.json")
+    if args.news32:
+        KERNEL_TAGS[:] = ["news_score32ILi0ELb0ELb0ELi24E", "news_score32<0, false, false, 24>"]
+        workload, kernel = "news_L50_K32_d768_C40_N104000_fp32", "news_score<fp32,weighted>"
+        if args.out == os.path.join(ROOT, "profiles", "pmc_traffic.json"):
+            args.out = os.path.join(ROOT, "profiles", "pmc_traffic_news_fp32.json")
     med, n = {}, {}
     for d in args.dirs:
         if not os.path.isdir(d):
@@ -86,8 +93,8 @@ def main():
         res["gpu_busy_cycles"] = gui
         res["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui * 4 * args.cus)
         res["mfma_instructions_32x32x16"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / 32
-    for c in ("SQ_BUSY_CU_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-        if c in med:
+    for c in sorted(med):
+        if c.startswith(("SQ_", "GRBM_")) and c not in res:
             res[c] = med[c]
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as f:
