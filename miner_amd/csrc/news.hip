@@ -1348,44 +1348,56 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       for (int j = 0; j < 4; ++j) reinterpret_cast<float*>(lg + (l0 + j) * 128)[k] = expf(x[j] - M) * inv;
     }
   };
-  // this lane's row offsets for item (i, pass): wave w DMAs rows 8w .. 8w+7 of each part; bit 0 of
-  // lv: history rows live (E, and proj when weighted), bit 1: candidate rows live
-  auto item_offsets = [&](int i, int pass, uint32_t& oH, uint32_t& oC, unsigned& lv) {
+  // this lane's row offsets for item (i, pass). The row DMAs are issued by the mui-path waves 0-3
+  // only (no GELU: the shorter compute), each two 8-row blocks b = 2 (w & 3) + jj of every part, so
+  // the X waves 4-7 start their products right after the barrier, alone on their SIMDs while the
+  // partner waits on the address path. lv bit jj: history rows of block jj live (E, and proj when
+  // weighted), bit 2 + jj: its candidate rows live
+  const bool dma8 = (p.abl & 64) != 0;   // experiment: every wave issues one block of each part
+  auto dma_block = [&](int jj) { return dma8 ? wave : 2 * (wave & 3) + jj; };
+  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC, unsigned& lv) {
     const int lane = threadIdx.x & 63;
-    const bool live = i < n_i;
+    const bool live = i < n_i && (dma8 || wave < 4);
     int off = 0, cnt = 1;
     if (live) cands(i, off, cnt);
     const int cntp = max(1, min(64, cnt - 64 * pass));
-    const int row0 = 8 * wave;
     lv = 0;
-    if (live && row0 < L) lv |= 1u;
-    if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 2u;
-    lv = __builtin_amdgcn_readfirstlane(lv);
-    const int prow = row0 + (lane >> 3);                    // the ring row this lane fills
-    const int rowp = X6 ? x6row(prow) : prow;                // the logical row it fetches
-    const uint32_t poff = (uint32_t)(((lane & 7) ^ (X6 ? x6swz(prow) : f32swz(rowp))) << 4);
-    int h = 0, c = 0;
-    if (live) {
-      h = l1_his(smem, i & 3)[min(rowp, L - 1)];
-      if (WITH_CAND) c = l1_cand(smem, i & 3)[min(64 * pass + min(rowp, cntp - 1), kMaxCand - 1)];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      if (dma8 && jj == 1) break;
+      const int row0 = 8 * dma_block(jj);
+      if (live && row0 < L) lv |= 1u << jj;
+      if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 4u << jj;
+      const int prow = row0 + (lane >> 3);                    // the ring row this lane fills
+      const int rowp = X6 ? x6row(prow) : prow;                // the logical row it fetches
+      const uint32_t poff = (uint32_t)(((lane & 7) ^ (X6 ? x6swz(prow) : f32swz(rowp))) << 4);
+      int h = 0, c = 0;
+      if (live) {
+        h = l1_his(smem, i & 3)[min(rowp, L - 1)];
+        if (WITH_CAND) c = l1_cand(smem, i & 3)[min(64 * pass + min(rowp, cntp - 1), kMaxCand - 1)];
+      }
+      h = min(max(h, 0), p.n_news - 1);
+      c = min(max(c, 0), p.n_news - 1);
+      const uint32_t rowBytes = (uint32_t)d * 4u;
+      oH[jj] = (uint32_t)h * rowBytes + poff;
+      oC[jj] = (uint32_t)c * rowBytes + poff;
     }
-    h = min(max(h, 0), p.n_news - 1);
-    c = min(max(c, 0), p.n_news - 1);
-    const uint32_t rowBytes = (uint32_t)d * 4u;
-    oH = (uint32_t)h * rowBytes + poff;
-    oC = (uint32_t)c * rowBytes + poff;
+    lv = __builtin_amdgcn_readfirstlane(lv);
   };
   const bool abl_nodma = (p.abl & 2) != 0, abl_nocomp = (p.abl & 4) != 0;   // timing ablations (outputs wrong)
   NS_STAMP_DECL
-  auto dma32 = [&](uint32_t oH, uint32_t oC, unsigned lv, int ich, int slot) {
-    if (abl_nodma) return;
-    const unsigned m = sbase + slot * Cf::SLOT + wave * 1024;
+  auto dma32 = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int ich, int slot) {
+    if (abl_nodma || lv == 0) return;
     const char* bE = tabB + ich * kF32CW * 4;
-    if (lv & 1u) {
-      dma_row(oH, bE, m);
-      if constexpr (WEIGHTED) dma_row(oH, prjB + ich * kF32CW * 4, m + Cf::PART);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const unsigned m = sbase + slot * Cf::SLOT + dma_block(jj) * 1024;
+      if (lv & (1u << jj)) {
+        dma_row(oH[jj], bE, m);
+        if constexpr (WEIGHTED) dma_row(oH[jj], prjB + ich * kF32CW * 4, m + Cf::PART);
+      }
+      if (lv & (4u << jj)) dma_row(oC[jj], bE, m + 2 * Cf::PART);
     }
-    if (lv & 2u) dma_row(oC, bE, m + 2 * Cf::PART);
   };
 
   // ---- per-lane LDS offsets (fixed for the launch) ----
@@ -1483,7 +1495,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     soft_phase(0, 2);
     raw_barrier();
   }
-  uint32_t cH, cC, nH = 0, nC = 0;
+  uint32_t cH[2], cC[2], nH[2] = {0u, 0u}, nC[2] = {0u, 0u};
   unsigned cLv = 0, nLv = 0;
   item_offsets(0, 0, cH, cC, cLv);
   dma32(cH, cC, cLv, 0, 0);
@@ -1495,13 +1507,14 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   int pend_off = -1, pend_cnt = 0;
   int t = 0;
 
-  // S7 on waves 0-3: wave w candidates [16w, 16w+16) of the finished pass, lane (kq, c) interests
+  // S7 on waves 4-7 (the X waves, which wait at the barrier otherwise): wave w candidates [16(w-4), +16) of the finished pass, lane (kq, c) interests
   // [8kq, 8kq+8); the 4 lane rows combined by permlanes (model.py:128-136, :213-214)
+  const bool s7lo = (p.abl & 128) != 0;  // experiment: S7 on waves 0-3
   auto s7 = [&]() {
-    if (wave >= 4) return;
+    if (s7lo ? wave >= 4 : wave < 4) return;
     const int lane = threadIdx.x & 63;
     const int cl = lane & 15, kq = lane >> 4;
-    const int c = 16 * wave + cl;
+    const int c = 16 * (wave & 3) + cl;
     const float* F0 = reinterpret_cast<const float*>(smem + kOffX + 16384);
     const float* F1 = F0 + 2048;
     const int sw = (c >> 1) & 31;
@@ -1788,7 +1801,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       }
       pend_off = c_off + 64 * cp;
       pend_cnt = cntp;
-      cH = nH; cC = nC; cLv = nLv;
+      cH[0] = nH[0]; cH[1] = nH[1]; cC[0] = nC[0]; cC[1] = nC[1]; cLv = nLv;
       NS_STAMP(7);
     }
   }
