@@ -490,9 +490,13 @@ static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>:
 
 // chunk swizzle of a slot row: bf16 (8 chunks per row, 2 rows per 256-byte bank row): rows 4q..4q+3
 // of a transposed read hit disjoint banks and 16 rows of a ds_read_b128 group distinct slots;
-// fp32 (16 chunks per row): row & 15
+// bf16 with 256-byte rows (CW = 128): chunk ^ ((row & 3) << 2 | (row >> 2) & 3) — the row & 15 of
+// the fp32 layout leaves the 32x32x16 transposed reads 4-way (cdna_hip_programming.md T10), this
+// XOR makes them and the candidate ds_read_b128 conflict-free (PMC: 2.9k conflict cycles per
+// impression before); fp32 (16 chunks per row): row & 15
 template <class T, int CW = 64> __device__ __forceinline__ int nswz(int row) {
   if constexpr (NCfg<T, CW>::PPR == 8) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+  else if constexpr (sizeof(T) == 2) return ((row & 3) << 2) | ((row >> 2) & 3);
   else return row & 15;
 }
 // A-operand fragment of a part's transpose: rows = columns 32 sl + pi(r) of the chunk, contraction
@@ -567,19 +571,20 @@ __device__ __forceinline__ void dma_row(uint32_t off, const char* base, unsigned
 // not issued (bit jj of `live`: history rows of E and proj; bit NI + jj: candidate rows). Those ring
 // rows keep the zeros written at kernel start (or a finite row of an earlier chunk): they meet only
 // A = 0 history slots and candidate rows whose scores are never stored. proj rows only for 'weighted'.
+// SKIP: instruction jj lands at mE + jj * jstep (the block map is the caller's).
 template <class T, int CW, bool SKIP, bool WITH_PROJ>
 __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC, const char* bE, const char* bY,
-                                          unsigned mE, unsigned live) {
+                                          unsigned mE, unsigned live, unsigned jstep = kWaves * 1024) {
   using Cf = NCfg<T, CW>;
   [[maybe_unused]] unsigned t;
   if constexpr (SKIP) {
 #pragma unroll
     for (int jj = 0; jj < Cf::NI; ++jj) {
       if (live & (1u << jj)) {
-        dma_row(oH[jj], bE, mE + jj * kWaves * 1024);
-        if constexpr (WITH_PROJ) dma_row(oH[jj], bY, mE + Cf::PART + jj * kWaves * 1024);
+        dma_row(oH[jj], bE, mE + jj * jstep);
+        if constexpr (WITH_PROJ) dma_row(oH[jj], bY, mE + Cf::PART + jj * jstep);
       }
-      if (live & (1u << (Cf::NI + jj))) dma_row(oC[jj], bE, mE + 2 * Cf::PART + jj * kWaves * 1024);
+      if (live & (1u << (Cf::NI + jj))) dma_row(oC[jj], bE, mE + 2 * Cf::PART + jj * jstep);
     }
   } else if constexpr (Cf::NI == 1) {
     asm volatile(
@@ -621,6 +626,11 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
   constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
   constexpr bool SKIP = PD == 1;              // padding-row DMAs not issued (dma_chunk)
+  // 128-column chunks (config 3): the second DMA block of wave w is block 8 + (w ^ 4), so the rows
+  // 32..47 (live for L = 50, C = 40) go to the X-path waves 4-7 and the rows 48..63 (mostly padding,
+  // not fetched) to the mui-path waves 0-3; S7 runs on waves 4-7. With the X waves prioritised the
+  // mui waves are the critical path: this moves 8 of the 36 live DMAs per chunk and S7 off it.
+  constexpr bool SWAP = SKIP && NSLAB == 4;
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int L = p.L, d = p.d;
@@ -628,6 +638,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   // cooperative softmax one impression ahead (always for 128-column chunks: the host picks them for d >= 512)
   const bool coop = CW == 128 || (nchunk >= PD + 1 && nchunk >= 4);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w4 = SWAP ? (wave ^ 4) : wave;
   const char* tabB = static_cast<const char*>(p.table);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
@@ -768,7 +779,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     lv = 0;                            // live DMA instructions of this wave (dma_chunk, SKIP)
 #pragma unroll
     for (int jj = 0; jj < NI; ++jj) {
-      const int row0 = (wave + 8 * jj) * Cf::RPI;   // first row of instruction jj
+      const int row0 = (jj ? w4 + 8 * jj : wave) * Cf::RPI;   // first row of instruction jj
       if (live && row0 < L) lv |= 1u << jj;
       if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 1u << (NI + jj);
     }
@@ -778,7 +789,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     const uint32_t rowBytes = (uint32_t)d * sizeof(T);
 #pragma unroll
     for (int jj = 0; jj < NI; ++jj) {
-      const int rowp = (wave + 8 * jj) * Cf::RPI + lane / Cf::PPR;
+      const int rowp = (jj ? w4 + 8 * jj : wave) * Cf::RPI + lane / Cf::PPR;
       const uint32_t poff = (uint32_t)(((lane % Cf::PPR) ^ nswz<T, CW>(rowp)) << 4);
       int h = 0, c = 0;
       if (live) {
@@ -930,7 +941,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
 #pragma unroll
   for (int k = 0; k < PD; ++k)
     dma_chunk<T, CW, SKIP, WEIGHTED>(cH, cC, tabB + k * CW * sizeof(T), prjB + k * CW * sizeof(T),
-                                     sbase + k * Cf::SLOT + wave * 1024, cLv);
+                                     sbase + k * Cf::SLOT + wave * 1024, cLv, (w4 + 8 - wave) * 1024);
 
   f32x16 acc[NT];                      // this wave's M / Lg partials, 32x32 candidate tiles
 #pragma unroll
@@ -942,10 +953,10 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   // pass, lane (kq, c) = (lane >> 4, lane & 15) interests [8 kq, 8 kq + 8); partials of the 8 waves
   // are summed here (M: waves ct, 2+ct; Lg: 4+ct, 6+ct), the 4 lane rows combined by permlanes
   auto s7 = [&]() {
-    if (wave >= 4) return;
+    if (SWAP ? wave < 4 : wave >= 4) return;
     const int lane = threadIdx.x & 63;
     const int cl = lane & 15, kq = lane >> 4;
-    const int c = 16 * wave + cl;              // candidate of the pass
+    const int c = 16 * (wave & 3) + cl;        // candidate of the pass
     const int tct = c >> 5, cr = c & 31;       // c-tile, row in the tile
     const float* X = reinterpret_cast<const float*>(smem + kOffX);
     const int sw = (cr >> 1) & 31;
@@ -1001,10 +1012,13 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   // one 64-column chunk: the row DMAs of chunk `ich` of the item whose offsets are (iH, iC), PD
   // chunks ahead, then the X / mui slab and the candidate product of this chunk.
   // `mode`: 1 X, 2 candidate product, 4 mui out
+  NS_STAMP_DECL
   auto chunk = [&](int ci, int cc, int mode, int ncand, const uint32_t* iH, const uint32_t* iC, unsigned iLv,
                    int ich) {
+    NS_STAMP(2);
     dma_chunk<T, CW, SKIP, WEIGHTED>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
-                                     sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024, iLv);
+                                     sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024, iLv, (w4 + 8 - wave) * 1024);
+    NS_STAMP(3);
     if (mode & 1) {
       FRESH_LANE_IDS();
       const char* slot = smem + (t & (NS - 1)) * Cf::SLOT;
@@ -1026,6 +1040,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         }
         mma_slab(ax, ef, af[ls]);
       }
+      NS_STAMP(4);
       if ((mode & 4) && r < p.K) {
         float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + r) * d + CW * cc + 32 * sl + 16 * h;
 #pragma unroll
@@ -1036,6 +1051,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         if (WEIGHTED && P == 1) gelu_tile<T>(ax);
         Frag<T> xf;
         acc_to_frag<T>(xf, ax);
+        NS_STAMP(5);
 #pragma unroll
         for (int tl = 0; tl < NT; ++tl) {
           if (tl == 0 || ncand > 32) {
@@ -1050,8 +1066,10 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   };
   auto wait_slot = [&]() {
     // slot t landed (this wave's DMAs: all but the PD-1 younger chunks), then for every wave
+    NS_STAMP(6);
     vm_wait<3 * NI * (PD - 1)>();
     raw_barrier();
+    NS_STAMP(0);
   };
 
   for (int ci = 0; ci < n_i; ++ci) {
@@ -1071,7 +1089,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       auto extras = [&](int cc) {
         if (cc == 0) {
           did_s7 = WITH_CAND && pend_off >= 0;
+          NS_STAMP(1);
           if (did_s7) s7();
+          NS_STAMP(7);
           pend_off = -1;
           if (cp == 0) {
             if (coop) {
@@ -1090,9 +1110,13 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         } else if (coop && cp == 0) {
           if (cc == 1) {
             issue_L2(ci + 2);          // into the rows A of ci was read from (free since the barrier)
+            NS_STAMP(1);
             soft_phase(ci + 1, 1);
+            NS_STAMP(2);
           } else if (cc == 2) {
+            NS_STAMP(1);
             soft_phase(ci + 1, 2);
+            NS_STAMP(2);
           }
         }
       };
@@ -1100,12 +1124,14 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       for (; cc < nchunk - PD; ++cc, ++t) {
         wait_slot();
         extras(cc);
+        NS_STAMP(1);
         chunk(ci, cc, mode, cntp, cH, cC, cLv, cc + PD);
       }
       item_offsets(ni, np, nH, nC, nLv);
       for (; cc < nchunk; ++cc, ++t) {
         wait_slot();
         extras(cc);
+        NS_STAMP(1);
         chunk(ci, cc, mode, cntp, nH, nC, nLv, cc + PD - nchunk);
       }
       // pass done: partials -> LDS blocks [c][k ^ swizzle] (block = 4P + 2 sl + tile for the two
@@ -1155,6 +1181,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   vm_wait_all();
   raw_barrier();
   if (WITH_CAND && pend_off >= 0) s7();
+  NS_STAMP_FLUSH(n_i);
 }
 
 // ================================================================================================

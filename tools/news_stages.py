@@ -17,12 +17,15 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 STAGES = ["vm_wait (row DMAs)", "barrier", "item start / softmax / aux", "DMA issue",
           "history product", "gelu + split", "candidate product", "pass end + loop"]
+STAGES16 = ["slot wait + barrier", "item start rest / aux", "softmax phases", "DMA issue", "history product",
+            "gelu + frag", "cand product + pass end", "S7"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--batch", type=int, default=32768)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     args = ap.parse_args()
     import stage_profile
     if args.build:
@@ -37,14 +40,15 @@ def main():
     dev = "cuda:0"
     B, n_news, L, C, d, K, Dc = args.batch, 104000, 50, 40, 768, 32, 200
     g = torch.Generator(device=dev).manual_seed(36)
-    table = torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    table = (torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5).to(dt)
     lens = torch.randint(0, L + 1, (B,), generator=g, device=dev)
     mask = torch.arange(L, device=dev)[None, :] >= (L - lens)[:, None]
     hid = torch.randint(1, n_news, (B, L), generator=g, device=dev, dtype=torch.int32)
     hid[~mask] = 0
     cid = torch.randint(1, n_news, (B, C), generator=g, device=dev, dtype=torch.int32)
     W1, Q, W2 = synthetic.init_weights(36, d, Dc, K, device=dev)
-    nt = news.precompute(table, ops.pack_weights(W1, Q, W2))
+    nt = news.precompute(table, ops.pack_weights(W1, Q, W2, dtype=dt))
     news.score(nt, hid, mask, cid, validate=False)
     out = (ctypes.c_ulonglong * 65)()
     fn(out)
@@ -58,10 +62,12 @@ def main():
     ms = a.elapsed_time(b) / reps
     assert fn(out) == 0
     n = out[64]
-    print(f"fp32 news_score32 ({'bf16x6' if os.environ.get('MINER_NEWS_F32X6') else 'fp32 MFMA'}) B={B}: "
+    kind = "bf16 news_score" if args.dtype == "bf16" else \
+        f"fp32 news_score32 ({'bf16x6' if os.environ.get('MINER_NEWS_F32X6') else 'fp32 MFMA'})"
+    print(f"{kind} B={B}: "
           f"{ms:.3f} ms/launch ({ms / B * 131072:.2f} ms per 131k), cycles per impression per workgroup:")
     print(f"  {'stage':28s}" + "".join(f"  wave{w}" for w in range(8)))
-    for i, name in enumerate(STAGES):
+    for i, name in enumerate(STAGES16 if args.dtype == "bf16" else STAGES):
         print(f"  {name:28s}" + "".join(f" {out[8 * w + i] / n:6.0f}" for w in range(8)))
     print(f"  {'total':28s}" + "".join(f" {sum(out[8 * w + i] for i in range(8)) / n:6.0f}" for w in range(8)))
 
