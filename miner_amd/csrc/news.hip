@@ -1259,7 +1259,15 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int L = p.L, d = p.d;
   const int nchunk = NCH > 0 ? NCH : d / kF32CW;
-  const bool coop = nchunk >= 6;                             // cooperative softmax one impression ahead
+  // softmax over the history (model.py:176-181): smode 2 (d >= 128): every wave computes its own A slice
+  // (16 interests) at the item's first pair, the next logit rows and softmax coefficients are staged
+  // at the second pair (the block it read is free after that barrier). An fp32 wave needs 16 exps per
+  // lane either way, and the cooperative form (smode 1, MINER_NEWS_ABL bit 256) adds two LDS round
+  // trips and a partial exchange; smode 0 (one pair per item): in-wave + a barrier before the L2 DMA
+  const int npair0 = nchunk >> 1;
+  const int smode = (p.abl & 256) && nchunk >= 6 ? 1 : (npair0 >= 2 ? 2 : 0);
+  const bool coop = smode == 1;
+  const bool split_f = npair0 >= 2 && !(p.abl & 512);    // pass end without a barrier (see the pass end)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const char* tabB = static_cast<const char*>(p.table);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
@@ -1544,13 +1552,19 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     const int c = 16 * (wave & 3) + cl;
     const float* F0 = reinterpret_cast<const float*>(smem + kOffX + 16384);
     const float* F1 = F0 + 2048;
+    const float* G = reinterpret_cast<const float*>(smem + kOffX);    // split_f: [P][ct] blocks of 2048
     const int sw = (c >> 1) & 31;
     float lg[8], m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int o = c * 32 + ((8 * kq + j) ^ sw);
-      m[j] = F0[o];
-      if constexpr (WEIGHTED) lg[j] = F1[o];
+      if (split_f) {
+        m[j] = G[o] + G[2048 + o];
+        if constexpr (WEIGHTED) lg[j] = G[4096 + o] + G[6144 + o];
+      } else {
+        m[j] = F0[o];
+        if constexpr (WEIGHTED) lg[j] = F1[o];
+      }
     }
     float sc;
     if constexpr (WEIGHTED) {
@@ -1762,8 +1776,10 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           if (WITH_CAND && pend_off >= 0) s7();
           pend_off = -1;
           if (cp == 0) {
-            if (coop) {
+            if (smode == 1) {
               load_aw(ci);
+            } else if (smode == 2) {
+              softmax_inwave(ci);
             } else {
               softmax_inwave(ci);
               raw_barrier();           // every wave has read impression ci's logit rows
@@ -1771,10 +1787,13 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
             }
             issue_L0(ci + 4);
             issue_L1(ci + 3);
-            prep_softmax(ci + 2);
+            if (smode != 2) prep_softmax(ci + 2);
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        } else if (smode == 2 && cp == 0 && u == 1) {
+          issue_L2(ci + 2);            // into the block impression ci's logits were read from
+          prep_softmax(ci + 2);
         } else if (coop && cp == 0) {
           if (u == 1) {
             issue_L2(ci + 2);          // into the rows A of ci was read from (free since the barrier)
@@ -1796,7 +1815,27 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         compute(ci, 2 * u, mode, ntile);
         NS_STAMP(6);
       }
-      if constexpr (WITH_CAND) {
+      if (WITH_CAND && split_f) {
+        // pass done (npair >= 2): every wave publishes its partial M / Lg [c][k ^ swizzle] into its
+        // own block F[P][ct], no barrier; S7, after the next pair's barrier, sums the two column-tile
+        // partials in the order of the hand-off below (ct 0 + ct 1). The next pass end is at least
+        // one barrier after that S7.
+        const int lane = threadIdx.x & 63;
+        const int j = lane & 15, g = lane >> 4;
+        if (path_live && k_live) {
+          float* F = reinterpret_cast<float*>(smem + kOffX) + (P * 2 + ct) * 2048;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (q < ntile) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int c = 16 * q + 4 * g + e;
+                F[c * 32 + ((16 * kt + j) ^ ((c >> 1) & 31))] = acc[q][e];
+              }
+            }
+          }
+        }
+      } else if constexpr (WITH_CAND) {
         // pass done: the ct = 1 waves hand their partials to the ct = 0 waves of the same (P, kt),
         // which publish the final M / Lg [c][k ^ swizzle] for S7
         const int lane = threadIdx.x & 63;
