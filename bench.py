@@ -405,6 +405,10 @@ def run_news(args, rank, world, dev):
     W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
     pool = [news_batch(36 + (rank * args.pool + p), B, N_NEWS, dev) for p in range(args.pool)]
     torch.cuda.synchronize()
+    # the dense-row comparison line first: measured after the minute of fp32 / bf16 news launches
+    # below it read 3.53-3.59 ms, in isolation every version of the kernel since round-1 v8 reads
+    # 3.26-3.37 ms (tools/bisect_dense.py, profiles/r02_dense_bisect.txt)
+    dense = dense_kernel_line(dev) if (world == 1 and not args.no_dense) else None
 
     # headline: fp32 (the reference's precision)
     el32, pre32, kern32, o32, nt32 = measure_news(table32, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
@@ -416,7 +420,6 @@ def run_news(args, rank, world, dev):
     s16 = o16[0]
     assert torch.isfinite(s16).all()
     c2 = config2_line(args, rank, world, dev) if not args.no_config2 else None
-    dense = dense_kernel_line(dev) if (world == 1 and not args.no_dense) else None
 
     if rank != 0:
         return
@@ -468,14 +471,15 @@ def run_news(args, rank, world, dev):
     print(json.dumps(line), flush=True)
 
 
-def dense_kernel_line(dev, B=32768, steps=5):
+def dense_kernel_line(dev, B=32768, steps=10):
     """The fused dense-row kernel (weights per impression, miner_score) on the same shape, for
     comparison: pairs/s and its MFMA fraction."""
     from miner_amd import ops, synthetic
     imp = synthetic.impressions(36, 0, B, L=L, d=D, C=C, device=dev, dtype=torch.bfloat16)
     W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
     pw = ops.pack_weights(W1, Q, W2, dtype=torch.bfloat16)
-    ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+    for _ in range(3):
+        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
