@@ -3,7 +3,7 @@
 * fp32 parity mode vs the reference's own outputs (tests/golden/fastformer_*.npz, made by running
   the reference FastFormer) and vs the oracle on random inputs: |x - ref| <= 1e-5|ref| + 1e-5·rms;
 * bf16 mode vs the oracle evaluated in fp32 on the SAME bf16-rounded inputs and weights:
-  |x - ref| <= 3e-2|ref| + 6e-2·rms (activations re-rounded to bf16 before each of the 13
+  |x - ref| <= 6e-3|ref| + 1.2e-2·rms (activations re-rounded to bf16 before each of the 13
   matrix products, LayerNorms in between);
 * gather == dense and ragged == dense bit-exactly (same rows, deterministic kernel);
 * the drop-in modules load the reference state_dict and reproduce its scores.
@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 HERE = os.path.dirname(os.path.abspath(__file__))
 NAMES = ["cfg4_slice", "edge_short", "edge_empty", "edge_full"]
-BF16_TOL = dict(rtol=3e-2, rms_floor=6e-2)
+BF16_TOL = dict(rtol=6e-3, rms_floor=1.2e-2)
 
 
 def load(name):

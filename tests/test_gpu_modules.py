@@ -5,7 +5,7 @@ PolyAttention.forward, TargetAwareAttention.forward — src/model/model.py:61-13
 Weights enter through ``load_state_dict`` with the reference's parameter names; ``Miner.forward``
 runs with the stub news encoder of make_golden.py (token 0 of a title is a news-table row).
 Tolerances as tests/test_gpu_parity.py: fp32 |x - ref| <= 1e-5·|ref| + 1e-5·rms(ref); bf16 mode
-against the oracle on the same bf16-rounded inputs and weights, 2e-2·|ref| + 6e-2·rms(ref).
+against the oracle on the same bf16-rounded inputs and weights, 7e-3·|ref| + 2e-2·rms(ref).
 """
 import numpy as np
 import pytest
@@ -142,7 +142,7 @@ def test_miner_score_bf16(name):
         mui, scores = m.score(E.to(DEV), torch.from_numpy(g["his_mask"]).to(DEV), Cd.to(DEV),
                               category_bias=None if bias is None else bias.to(DEV))
     torch.cuda.synchronize()
-    ok, worst = orc.parity_ok(scores.cpu().numpy(), rs.numpy(), rtol=2e-2, rms_floor=6e-2)
+    ok, worst = orc.parity_ok(scores.cpu().numpy(), rs.numpy(), rtol=7e-3, rms_floor=2e-2)
     assert ok, f"{name}: bf16 scores off by {worst:.2f}x the bf16 tolerance"
 
 

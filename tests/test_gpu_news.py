@@ -5,8 +5,8 @@ outputs (golden fixtures, fp32) and the oracle, never bit-for-bit against the de
 
 Tolerances (as tests/test_gpu_parity.py):
 * fp32: |x - ref| <= 1e-5*|ref| + 1e-5*rms(ref)   (north_star 1e-5 relative + SURVEY §8c floor)
-* bf16: against the oracle on the same bf16-rounded table and weights, |x - ref| <= 2e-2*|ref| +
-  6e-2*rms(ref) (the kernel rounds the attention weights, proj rows and the GELU output to bf16
+* bf16: against the oracle on the same bf16-rounded table and weights, |x - ref| <= 7e-3*|ref| +
+  2e-2*rms(ref) (the kernel rounds the attention weights, proj rows and the GELU output to bf16
   MFMA operands).
 """
 import numpy as np
@@ -19,7 +19,7 @@ from tests.conftest import golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-BF_RTOL, BF_FLOOR = 2e-2, 6e-2
+BF_RTOL, BF_FLOOR = 7e-3, 2e-2
 
 
 def _dev(a, dtype=None):

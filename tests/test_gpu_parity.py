@@ -5,7 +5,8 @@ Tolerances:
   SURVEY.md §8c absolute floor for near-zero scores).
 * bf16 mode: compared with the oracle evaluated in fp32 on the SAME bf16-rounded inputs and weights;
   the kernel also rounds its on-chip intermediates (tanh(E·W1ᵀ), attention weights, mui, gelu
-  output) to bf16 MFMA operands, so the bound is |x - ref| <= 2e-2*|ref| + 6e-2*rms(ref), and the
+  output) to bf16 MFMA operands, so the bound is |x - ref| <= 7e-3*|ref| + 2e-2*rms(ref) (3x tighter
+  than round 1, set from the observed worst case: profiles/r02_tolerance_margins.txt), and the
   AUC computed from bf16 scores must stay within 5e-3 of the fp32 AUC.
 """
 import numpy as np
@@ -87,7 +88,7 @@ def test_bf16_within_tolerance(name):
                              _bf16_round(g["W1"]), _bf16_round(g["Q"]),
                              _bf16_round(g["W2"]) if "W2" in g else None, g["score_type"],
                              torch.from_numpy(g["bias"]) if g["use_bias"] else None)
-    ok, worst = orc.parity_ok(scores.cpu().numpy(), ref.numpy(), rtol=2e-2, rms_floor=6e-2)
+    ok, worst = orc.parity_ok(scores.cpu().numpy(), ref.numpy(), rtol=7e-3, rms_floor=2e-2)
     assert ok, f"{name}: bf16 scores off by {worst:.2f}x the bf16 tolerance"
 
 
