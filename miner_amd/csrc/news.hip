@@ -1773,13 +1773,16 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         raw_barrier();                 // then for every wave; the previous pair's slots are free
         NS_STAMP(1);
         if (u == 0) {
+          if (!X6) NS_STAMP(2);
           if (WITH_CAND && pend_off >= 0) s7();
+          if (!X6) NS_STAMP(4);          // fp32-MFMA form: stage 4 = S7, stage 5 = in-wave softmax
           pend_off = -1;
           if (cp == 0) {
             if (smode == 1) {
               load_aw(ci);
             } else if (smode == 2) {
               softmax_inwave(ci);
+              if (!X6) NS_STAMP(5);
             } else {
               softmax_inwave(ci);
               raw_barrier();           // every wave has read impression ci's logit rows

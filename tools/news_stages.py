@@ -67,7 +67,10 @@ def main():
     print(f"{kind} B={B}: "
           f"{ms:.3f} ms/launch ({ms / B * 131072:.2f} ms per 131k), cycles per impression per workgroup:")
     print(f"  {'stage':28s}" + "".join(f"  wave{w}" for w in range(8)))
-    for i, name in enumerate(STAGES16 if args.dtype == "bf16" else STAGES):
+    names = STAGES16 if args.dtype == "bf16" else STAGES
+    if args.dtype == "fp32" and not os.environ.get("MINER_NEWS_F32X6"):
+        names = STAGES[:4] + ["S7", "in-wave softmax", "products (history + candidate)", STAGES[7]]
+    for i, name in enumerate(names):
         print(f"  {name:28s}" + "".join(f" {out[8 * w + i] / n:6.0f}" for w in range(8)))
     print(f"  {'total':28s}" + "".join(f" {sum(out[8 * w + i] for i in range(8)) / n:6.0f}" for w in range(8)))
 
