@@ -231,6 +231,24 @@ __device__ __forceinline__ f32x4 mma_x6(f32x4 c, const Split8& a, const Split8& 
   return mfma16_bf16(a.hi, b.hi, c);
 }
 
+// The fp32 kernels' GELU at fewer VALU: Abramowitz & Stegun 7.1.26, erf(z) = 1 - t·P5(t)·e^{-z²},
+// t = 1/(1 + 0.3275911 z), |Δerf| <= 1.5e-7 for every z >= 0, so |Δgelu| <= 0.75e-7·|x| plus the
+// fp32 rounding: <= 2.2e-7·max(1, |x|) against float64 (tools/gelu_error.py), the accuracy class of
+// gelu_erfc_nr in ~13 VALU + rcp + exp instead of ~19 + rcp + exp.
+__device__ __forceinline__ float gelu_as_f32(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, z, 1.0f));
+  float q = __builtin_fmaf(1.061405429f, t, -1.453152027f);
+  q = __builtin_fmaf(q, t, 1.421413741f);
+  q = __builtin_fmaf(q, t, -0.284496736f);
+  q = __builtin_fmaf(q, t, 0.254829592f);
+  q *= t;
+  const float e = __builtin_amdgcn_exp2f(-1.4426950408889634f * (z * z));
+  const float erfz = __builtin_fmaf(-q, e, 1.0f);
+  const float hx = 0.5f * x;
+  return __builtin_fmaf(hx, copysignf(erfz, x), hx);
+}
+
 // bf16-mode transcendentals: branch-free, a handful of VALU ops each.  Their error (tanh: a few
 // fp32 ulp of 1; erf: <= 1.5e-7 absolute, Abramowitz & Stegun 7.1.26) is far below the bf16
 // operand rounding of that mode.  The fp32 parity mode uses the libm tanhf / erff / expf.

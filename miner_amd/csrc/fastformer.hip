@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/miner_fastformer.h"
 #include "cdna4_common.h"
@@ -159,6 +160,7 @@ struct FfParams {
   float* scores;             // [sum C_b] or null
   float* user_out;           // [B, 256] or null
   int B, L, C, n_news;
+  int abl;                   // experiment bits (MINER_FF_ABL): 1 = static priority for waves 4-7
 };
 
 // LDS carve (bytes): two activation images | LN / pooler exchange | head softmax weights | user
@@ -593,6 +595,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
   const T* __restrict__ hist = static_cast<const T*>(p.hist);
   const int L = p.L;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if ((p.abl & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   FF_STAMP_DECL
   int n_done = 0;
 
@@ -922,7 +925,10 @@ int launch(void* stream, const FfParams& prm) {
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
-int run(void* stream, int dtype, const FfParams& prm) {
+int run(void* stream, int dtype, const FfParams& prm_in) {
+  FfParams prm = prm_in;
+  const char* abl = getenv("MINER_FF_ABL");
+  prm.abl = abl ? atoi(abl) : 0;
   const bool gather = prm.his_ids != nullptr;
   if (dtype == MINER_DTYPE_BF16) return gather ? launch<__bf16, true>(stream, prm) : launch<__bf16, false>(stream, prm);
   return gather ? launch<float, true>(stream, prm) : launch<float, false>(stream, prm);

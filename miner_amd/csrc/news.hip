@@ -1643,8 +1643,13 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         cf1[q] = *reinterpret_cast<const f32x4v*>(s1 + 2 * Cf::PART + cOff + q * 2048);
       }
       if (WEIGHTED && P == 1 && !(p.abl & 8)) {
+        if (p.abl & 2048) {            // A/B: the Numerical Recipes erfc form
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x0[e] = gelu_erfc_nr(x0[e]);
+          for (int e = 0; e < 4; ++e) x0[e] = gelu_erfc_nr(x0[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x0[e] = gelu_as_f32(x0[e]);
+        }
       }
       if (p.abl & 16) {
 #pragma unroll
@@ -1656,8 +1661,13 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(cf0[q][e], x0[e], acc[q], 0, 0, 0);
         }
         if (WEIGHTED && P == 1 && !(p.abl & 8)) {
+          if (p.abl & 2048) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) x1[e] = gelu_erfc_nr(x1[e]);
+            for (int e = 0; e < 4; ++e) x1[e] = gelu_erfc_nr(x1[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x1[e] = gelu_as_f32(x1[e]);
+          }
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1711,7 +1721,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       }
       if (WEIGHTED && P == 1 && !(p.abl & 8)) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = gelu_erfc_nr(x[i]);
+        for (int i = 0; i < 8; ++i) x[i] = gelu_as_f32(x[i]);
       }
       const Split8 sb = split8(x);
       NS_STAMP(5);

@@ -9,3 +9,8 @@ import gelu_error  # noqa: E402
 
 def test_gelu_erfc_nr_error_bound():
     assert gelu_error.max_error() <= 2e-7
+
+
+def test_gelu_as_f32_error_bound():
+    """gelu_as_f32 (Abramowitz & Stegun 7.1.26) in the device's operation order: <= 2.5e-7·max(1, |x|)."""
+    assert gelu_error.max_error(gelu_error.gelu_as) <= 2.5e-7

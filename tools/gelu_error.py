@@ -25,14 +25,30 @@ def gelu_nr(x):
     return f32(x * phi)
 
 
-def max_error():
+def gelu_as(x):
+    """cdna4_common.h gelu_as_f32 (Abramowitz & Stegun 7.1.26 erf) in the device's operation order."""
+    x = f32(x)
+    z = f32(abs(x) * f32(0.70710678118654752440))
+    t = f32(1) / f32(f32(f32(0.3275911) * z) + f32(1))
+    q = f32(f32(f32(1.061405429) * t) + f32(-1.453152027))
+    for k in (1.421413741, -0.284496736, 0.254829592):
+        q = f32(f32(q * t) + f32(k))
+    q = f32(q * t)
+    e = f32(np.exp2(f32(f32(-1.4426950408889634) * f32(z * z))))
+    erfz = f32(f32(1) - f32(q * e))
+    hx = f32(f32(0.5) * x)
+    return f32(f32(hx * f32(np.copysign(erfz, x))) + hx)
+
+
+def max_error(fn=gelu_nr):
     xs = np.concatenate([np.linspace(-10, 10, 200001), np.logspace(-8, 1, 2000), -np.logspace(-8, 1, 2000)])
     worst = 0.0
     for x in xs:
         ref = 0.5 * x * erfc(-x / sqrt(2))
-        worst = max(worst, abs(float(gelu_nr(x)) - ref) / max(1.0, abs(x)))
+        worst = max(worst, abs(float(fn(x)) - ref) / max(1.0, abs(x)))
     return worst
 
 
 if __name__ == "__main__":
-    print(f"max |gelu_nr - gelu| / max(1, |x|) = {max_error():.3e}")
+    print(f"max |gelu_nr - gelu| / max(1, |x|) = {max_error(gelu_nr):.3e}")
+    print(f"max |gelu_as - gelu| / max(1, |x|) = {max_error(gelu_as):.3e}")
