@@ -1618,17 +1618,24 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       a0[s] = *reinterpret_cast<const float*>(s0 + P * Cf::PART + hOff[s & 1] + (s >> 1) * 1024);
       a1[s] = *reinterpret_cast<const float*>(s1 + P * Cf::PART + hOff[s & 1] + (s >> 1) * 1024);
     }
-    // one fma chain per chunk, the two chunks' chains interleaved, each starting on a zero
-    // accumulator operand (inline constant, no register zeroing). Against even / odd chains summed at
-    // the end (four chains, 8 VALU adds): -2.3 % in an interleaved A/B
+    // two fma chains per chunk (even / odd steps: four independent chains across the pair against
+    // the 40-cycle dependent latency of the 16x16x4 f32 MFMA), each starting on a zero accumulator
+    // operand (inline constant, no register zeroing). One chain per chunk: +5 % (tools/bisect_news.py)
     const f32x4v z4 = f32x4v{0.f, 0.f, 0.f, 0.f};
-    f32x4v x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], aw[0], z4, 0, 0, 0);
-    f32x4v x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], aw[0], z4, 0, 0, 0);
+    f32x4v h00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], aw[0], z4, 0, 0, 0);
+    f32x4v h10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], aw[0], z4, 0, 0, 0);
+    f32x4v h01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], aw[1], z4, 0, 0, 0);
+    f32x4v h11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], aw[1], z4, 0, 0, 0);
 #pragma unroll
-    for (int s = 1; s < NST; ++s) {
-      x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], aw[s], x0, 0, 0, 0);
-      x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], aw[s], x1, 0, 0, 0);
+    for (int s = 2; s < NST; s += 2) {
+      h00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], aw[s], h00, 0, 0, 0);
+      h10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], aw[s], h10, 0, 0, 0);
+      if (s + 1 < NST) {
+        h01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s + 1], aw[s + 1], h01, 0, 0, 0);
+        h11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s + 1], aw[s + 1], h11, 0, 0, 0);
+      }
     }
+    const f32x4v x0 = h00 + h01, x1 = h10 + h11;
     if ((mode & 4) && 16 * kt + j < p.K) {
       float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + 16 * kt + j) * d + kF32CW * cc0 + 16 * ct + 4 * g;
       *reinterpret_cast<float4*>(dst) = make_float4(x0[0], x0[1], x0[2], x0[3]);
