@@ -1635,7 +1635,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         h11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s + 1], aw[s + 1], h11, 0, 0, 0);
       }
     }
-    const f32x4v x0 = h00 + h01, x1 = h10 + h11;
+    f32x4v x0 = h00 + h01, x1 = h10 + h11;
     if ((mode & 4) && 16 * kt + j < p.K) {
       float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + 16 * kt + j) * d + kF32CW * cc0 + 16 * ct + 4 * g;
       *reinterpret_cast<float4*>(dst) = make_float4(x0[0], x0[1], x0[2], x0[3]);
