@@ -1618,16 +1618,13 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       a0[s] = *reinterpret_cast<const float*>(s0 + P * Cf::PART + hOff[s & 1] + (s >> 1) * 1024);
       a1[s] = *reinterpret_cast<const float*>(s1 + P * Cf::PART + hOff[s & 1] + (s >> 1) * 1024);
     }
-    // two fma chains per chunk (even / odd steps: four independent chains across the pair against
-    // the 40-cycle dependent latency of the 16x16x4 f32 MFMA), each starting on a zero accumulator
-    // operand (inline constant, no register zeroing). One chain per chunk: +5 % (tools/bisect_news.py)
-    const f32x4v z4 = f32x4v{0.f, 0.f, 0.f, 0.f};
-    f32x4v h00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], aw[0], z4, 0, 0, 0);
-    f32x4v h10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], aw[0], z4, 0, 0, 0);
-    f32x4v h01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], aw[1], z4, 0, 0, 0);
-    f32x4v h11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], aw[1], z4, 0, 0, 0);
+    f32x4v h00 = f32x4v{0.f, 0.f, 0.f, 0.f}, h01 = h00, h10 = h00, h11 = h00;
+    // (the ablation branch below also shapes the schedule: without it, and with the chains
+    // started on an inline-zero accumulator instead, the kernel measured 7 % slower in a clean
+    // per-commit A/B, tools/bisect_news.py; one chain per chunk +5 %)
+    if (p.abl & 32) { h00[0] = a0[0]; h10[0] = a1[0]; } else
 #pragma unroll
-    for (int s = 2; s < NST; s += 2) {
+    for (int s = 0; s < NST; s += 2) {
       h00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], aw[s], h00, 0, 0, 0);
       h10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], aw[s], h10, 0, 0, 0);
       if (s + 1 < NST) {
