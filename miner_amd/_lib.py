@@ -48,6 +48,10 @@ SIGNATURES = {
     "miner_news_precompute": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _P]),
     "miner_score_news": (_I, [_P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "miner_news_supported": (_I, [_I, _I, _I, _I, _I]),
+    # include/miner_wide.h
+    "miner_score_wide": (_I, [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P]),
+    "miner_wide_proj": (_I, [_P, _I, _P, _P, _I, _I, _P]),
+    "miner_wide_supported": (_I, [_I, _I, _I, _I, _I]),
     # include/miner_metrics.h
     "miner_impression_metrics": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, _P]),
     "miner_auc_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),

@@ -16,6 +16,8 @@ import torch
 from . import _lib
 
 _DTYPES = {torch.float32: _lib.DTYPE_F32, torch.bfloat16: _lib.DTYPE_BF16}
+FUSED_MAX_K, FUSED_MAX_L = 32, 64       # miner_fused (miner_score.h); past them: the wide path
+WIDE_MAX_K, WIDE_MAX_L = 64, 256        # miner_encode_users + miner_score_wide (miner_wide.h)
 
 
 def _ptr(t):
@@ -57,13 +59,19 @@ def check_offsets(cand_offsets: torch.Tensor, B: int, N: int) -> None:
 
 @dataclasses.dataclass
 class PackedWeights:
-    """miner_pack_weights() output: one device buffer holding W1, Q and W2 in the kernel layout."""
-    buf: torch.Tensor
+    """miner_pack_weights() output: one device buffer holding W1, Q and W2 in the kernel layout.
+
+    ``buf`` is None when (d, Dc, K) is past the fused kernel (K > 32): such weights are scored by
+    the wide path (include/miner_wide.h), whose user-encoder pack is built from ``src`` on first use.
+    """
+    buf: torch.Tensor | None
     dtype: torch.dtype
     d: int
     Dc: int
     K: int
     has_target: bool
+    src: tuple | None = None                     # (w_poly, context_codes, w_target), dtype, detached
+    wide: object | None = dataclasses.field(default=None, repr=False)   # corpus.EncoderWeights cache
 
 
 def pack_weights(w_poly: torch.Tensor, context_codes: torch.Tensor, w_target: torch.Tensor | None = None,
@@ -82,14 +90,18 @@ def pack_weights(w_poly: torch.Tensor, context_codes: torch.Tensor, w_target: to
         raise ValueError(f"context_codes must be [K,{Dc}], got {tuple(q.shape)}")
     if w2 is not None and tuple(w2.shape) != (d, d):
         raise ValueError(f"w_target must be [{d},{d}], got {tuple(w2.shape)}")
+    src = tuple(None if t is None else t.detach() for t in (w1, q, w2))
     nbytes = _lib.lib().miner_packed_weights_bytes(dt, d, Dc, K)
     if nbytes == 0:
-        raise ValueError(f"weights d={d} Dc={Dc} K={K} not supported by this build")
+        if _lib.lib().miner_wide_supported(dt, 1, d, Dc, K) != 0:
+            raise ValueError(f"weights d={d} Dc={Dc} K={K} not supported by this build "
+                             f"(K <= {WIDE_MAX_K}, Dc <= 256, d <= 768)")
+        return PackedWeights(None, dtype, d, Dc, K, w2 is not None, src)      # wide path only
     buf = torch.empty(nbytes, dtype=torch.uint8, device=w1.device)
     with torch.cuda.device(w1.device):
         rc = _lib.lib().miner_pack_weights(_stream(w1.device), dt, _ptr(w1), _ptr(q), _ptr(w2), d, Dc, K, _ptr(buf))
     _lib.check(rc, "miner_pack_weights")
-    return PackedWeights(buf, dtype, d, Dc, K, w2 is not None)
+    return PackedWeights(buf, dtype, d, Dc, K, w2 is not None, src)
 
 
 def pack_target_weights(w_target: torch.Tensor, dtype: torch.dtype | None = None) -> PackedWeights:
@@ -109,7 +121,7 @@ def pack_target_weights(w_target: torch.Tensor, dtype: torch.dtype | None = None
     with torch.cuda.device(w2.device):
         rc = _lib.lib().miner_pack_target_weights(_stream(w2.device), dt, _ptr(w2), d, _ptr(buf))
     _lib.check(rc, "miner_pack_target_weights")
-    return PackedWeights(buf, dtype, d, 0, 0, True)
+    return PackedWeights(buf, dtype, d, 0, 0, True, (None, None, w2.detach()))
 
 
 def _check_mask_bias(his_mask: torch.Tensor, his_bias, B: int, L: int):
@@ -133,6 +145,56 @@ def _as_packed(w_poly, context_codes, w_target, dtype) -> PackedWeights:
             raise TypeError(f"packed weights are {w_poly.dtype}, activations {dtype}")
         return w_poly
     return pack_weights(w_poly, context_codes, w_target, dtype=dtype)
+
+
+def _fused_or_wide(dt: int, L: int, d: int, Dc: int, K: int) -> bool:
+    """True when the fused kernel takes the shape, False when the wide path does; raises when
+    neither does (the reference itself has no limit: model.py:18-21, :159-185)."""
+    code = _lib.lib().miner_supported(dt, L, d, Dc, K)
+    if code == 0:
+        return True
+    if _lib.lib().miner_wide_supported(dt, L, d, Dc, K) == 0:
+        return False
+    raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()} "
+                     f"(fused kernel: L <= {FUSED_MAX_L}, K <= {FUSED_MAX_K}; wide path: L <= {WIDE_MAX_L}, "
+                     f"K <= {WIDE_MAX_K}, Dc <= 256, d <= 768)")
+
+
+def _wide_encoder(pw: PackedWeights):
+    """The user-encoder pack (miner_encoder_pack, corpus.h) of these weights, built once."""
+    if pw.wide is None:
+        if pw.src is None or pw.src[0] is None:
+            raise ValueError("these packed weights carry no PolyAttention source tensors for the wide path")
+        from . import corpus
+        pw.wide = corpus.pack_encoder(pw.src[0], pw.src[1], pw.src[2], dtype=pw.dtype)
+    return pw.wide
+
+
+def _score_wide(pw: PackedWeights, st: int, rows: torch.Tensor, his_ids, mask_u8: torch.Tensor, his_bias,
+                cand: torch.Tensor, cand_ids, offs, B: int, C: int, n_out: int, return_user: bool):
+    """Wide path (include/miner_wide.h): miner_encode_users (PolyAttention and, for 'weighted',
+    gelu(mui·W2ᵀ); model.py:159-185, :212) then miner_score_wide (model.py:127-136, :213-214)."""
+    from . import corpus
+    enc = _wide_encoder(pw)
+    weighted = st == _lib.SCORE_WEIGHTED
+    if weighted and not enc.has_target:
+        raise ValueError("score_type='weighted' needs weights packed with w_target")
+    f32 = pw.dtype == torch.float32
+    res = corpus.encode_users(rows, mask_u8.view(torch.bool), enc, his_ids=his_ids, his_bias=his_bias,
+                              with_proj=weighted, return_f32=return_user and not f32)
+    mui, proj = res[0], res[1]
+    d, K = pw.d, pw.K
+    dev = rows.device
+    shape = (B, C) if offs is None else (n_out,)
+    scores = torch.empty(shape, device=dev, dtype=torch.float32)
+    n_news = rows.shape[0] if cand_ids is not None else 0
+    with torch.cuda.device(dev):
+        rc = _lib.lib().miner_score_wide(_stream(dev), _dtype_code(pw.dtype), st, _ptr(mui), _ptr(proj), _ptr(cand),
+                                         _ptr(cand_ids), n_news, _ptr(offs), None, B, C, d, K, _ptr(scores))
+    _lib.check(rc, "miner_score_wide")
+    if return_user:
+        return scores, (mui if f32 else res[2])
+    return scores
 
 
 def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tensor,
@@ -164,12 +226,11 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
         K, Dc = context_codes.shape
         if tuple(w_poly.shape) != (Dc, d):
             raise ValueError(f"w_poly must be [{Dc},{d}], got {tuple(w_poly.shape)}")
-    code = _lib.lib().miner_supported(dt, L, d, Dc, K)
-    if code != 0:
-        raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
+    fused = _fused_or_wide(dt, L, d, Dc, K)
     if st == _lib.SCORE_WEIGHTED and not isinstance(w_poly, PackedWeights) and w_target is None:
         raise ValueError("score_type='weighted' needs w_target (target_aware_attn.linear.weight)")
     pw = _as_packed(w_poly, context_codes, w_target if st == _lib.SCORE_WEIGHTED else None, tdt)
+    fused = fused and pw.buf is not None
     if pw.d != d:
         raise ValueError(f"packed weights are for d={pw.d}, history has d={d}")
     if pw.Dc == 0:
@@ -191,6 +252,9 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
             check_offsets(offs, B, candidates.shape[0])
         C = 0
         scores = torch.empty((candidates.shape[0],), device=history.device, dtype=torch.float32)
+    if not fused:
+        return _score_wide(pw, st, history, None, mask, his_bias, candidates, None, offs, B, C,
+                           scores.numel(), return_user)
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32) if return_user else None
     with torch.cuda.device(history.device):
         rc = _lib.lib().miner_score(_stream(history.device), dt, st, _ptr(history), _ptr(mask), _ptr(his_bias),
@@ -233,12 +297,11 @@ def score_gather(news_table: torch.Tensor, his_ids: torch.Tensor, his_mask: torc
         Dc, K = w_poly.Dc, w_poly.K
     else:
         K, Dc = context_codes.shape
-    code = _lib.lib().miner_supported(dt, L, d, Dc, K)
-    if code != 0:
-        raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
+    fused = _fused_or_wide(dt, L, d, Dc, K)
     if st == _lib.SCORE_WEIGHTED and not isinstance(w_poly, PackedWeights) and w_target is None:
         raise ValueError("score_type='weighted' needs w_target (target_aware_attn.linear.weight)")
     pw = _as_packed(w_poly, context_codes, w_target if st == _lib.SCORE_WEIGHTED else None, tdt)
+    fused = fused and pw.buf is not None
     if pw.d != d:
         raise ValueError(f"packed weights are for d={pw.d}, the news table has d={d}")
     if pw.Dc == 0:
@@ -263,6 +326,8 @@ def score_gather(news_table: torch.Tensor, his_ids: torch.Tensor, his_mask: torc
     if validate:
         _check_ids(hid, n_news, "his_ids")
         _check_ids(cid, n_news, "cand_ids")
+    if not fused:
+        return _score_wide(pw, st, table, hid, mask, his_bias, table, cid, offs, B, C, scores.numel(), return_user)
     mui = torch.empty((B, K, d), device=table.device, dtype=torch.float32) if return_user else None
     with torch.cuda.device(table.device):
         rc = _lib.lib().miner_score_gather(_stream(table.device), dt, st, _ptr(table), n_news, _ptr(hid), _ptr(mask),
@@ -287,9 +352,11 @@ def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly, contex
     if pw.d != d or Dc == 0:
         raise ValueError(f"packed weights are for d={pw.d} (Dc={Dc}), history has d={d}")
     mask, his_bias = _check_mask_bias(his_mask, his_bias, B, L)
-    code = _lib.lib().miner_supported(dt, L, d, Dc, K)
-    if code != 0:
-        raise ValueError(f"shape L={L} d={d} Dc={Dc} K={K}: {_lib.lib().miner_strerror(code).decode()}")
+    if not _fused_or_wide(dt, L, d, Dc, K) or pw.buf is None:
+        from . import corpus
+        res = corpus.encode_users(history, mask.view(torch.bool), _wide_encoder(pw), his_bias=his_bias,
+                                  with_proj=False, return_f32=tdt != torch.float32)
+        return res[0] if tdt == torch.float32 else res[2]
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32)
     with torch.cuda.device(history.device):
         rc = _lib.lib().miner_score(_stream(history.device), dt, _lib.SCORE_NONE, _ptr(history), _ptr(mask),
@@ -341,6 +408,24 @@ def target_aware(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, w_
             check_offsets(offs, B, key.shape[0])
         C = 0
         out = torch.empty((key.shape[0],), device=query.device, dtype=torch.float32)
+    if K > FUSED_MAX_K:
+        # wide path: proj = gelu(query · W2ᵀ) (model.py:212), then the weighted aggregation of the given
+        # value (model.py:213-214) — include/miner_wide.h
+        if K > WIDE_MAX_K or d % 64:
+            raise ValueError(f"TargetAwareAttention with K={K} d={d}: K <= {WIDE_MAX_K} and d % 64 == 0 past K = "
+                             f"{FUSED_MAX_K}")
+        w2 = pw.src[2] if pw.src is not None else None
+        if w2 is None:
+            raise ValueError("these packed weights carry no w_target source tensor for K > 32")
+        proj = torch.empty_like(query)
+        with torch.cuda.device(query.device):
+            rc = _lib.lib().miner_wide_proj(_stream(query.device), dt, _ptr(query), _ptr(_contig(w2, tdt)), B * K, d,
+                                            _ptr(proj))
+            _lib.check(rc, "miner_wide_proj")
+            rc = _lib.lib().miner_score_wide(_stream(query.device), dt, _lib.SCORE_WEIGHTED, None, _ptr(proj),
+                                             _ptr(key), None, 0, _ptr(offs), _ptr(value), B, C, d, K, _ptr(out))
+        _lib.check(rc, "miner_score_wide")
+        return out
     with torch.cuda.device(query.device):
         rc = _lib.lib().miner_target_aware(_stream(query.device), dt, _ptr(query), _ptr(key), _ptr(value), _ptr(offs),
                                            _ptr(pw.buf), pw.Dc, B, C, d, K, _ptr(out))

@@ -25,6 +25,21 @@ def golden_names():
                   if not os.path.basename(p).startswith(("reader_", "fastformer_", "corpus_")))
 
 
+def news_golden_names():
+    """The fixtures inside the news path's limits (L <= 64, K <= 32 with K % 4 == 0): the wide_*
+    fixtures (K up to 64, L up to 120) go through the wide path instead (include/miner_wide.h)."""
+    out = []
+    for n in golden_names():
+        z = np.load(os.path.join(GOLDEN_DIR, n + ".npz"), allow_pickle=False)
+        if int(z["L"]) <= 64 and int(z["K"]) <= 32 and int(z["K"]) % 4 == 0:
+            out.append(n)
+    return out
+
+
+def wide_golden_names():
+    return [n for n in golden_names() if n.startswith("wide_")]
+
+
 def load_golden(name):
     z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
     g = {k: z[k] for k in z.files}

@@ -2,7 +2,7 @@
 
 Run in the build container (the only place /root/reference exists):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case ...]
 
 It imports the reference's own ``src.model.model.Miner`` (src/model/model.py:13-138) with a stub
 news encoder (an embedding-table lookup: the north_star path starts from precomputed news
@@ -53,8 +53,12 @@ def main():
         def forward(self, title_encoding, title_attn_mask, sapo_encoding=None, sapo_attn_mask=None):
             return self.table[title_encoding[:, 0]]
 
+    only = set(sys.argv[1:])          # case names to (re)generate; all when empty
+
     def run_case(name, *, B, L, K, d, Dc, C, score_type="weighted", seed=0, use_bias=False,
                  hist_len=None, ties=False, n_cat=12, cat_dim=16):
+        if only and name not in only:
+            return
         rng = np.random.default_rng(seed)
         n_news = 1 + B * (L + C)
         table = (rng.standard_normal((n_news, d)) / np.sqrt(d)).astype(np.float32)
@@ -187,6 +191,12 @@ def main():
     run_case("edge_bias", B=12, L=20, K=8, d=64, Dc=32, C=5, seed=8, use_bias=True)
     # exact score ties (unstable argsort in mrr/ndcg, stable sort in hit@k)
     run_case("edge_ties", B=40, L=10, K=4, d=64, Dc=16, C=8, seed=9, ties=True)
+    # reference-legal shapes past the fused kernels' K <= 32 / L <= 64 (the wide path): K = 64 with a
+    # 120-long history, K = 40 (not a multiple of 16) with L = 80, and the bias path at L = 70
+    run_case("wide_k64_l120", B=6, L=120, K=64, d=256, Dc=64, C=12, seed=10)
+    run_case("wide_k40_l80_max", B=8, L=80, K=40, d=128, Dc=48, C=9, score_type="max", seed=11)
+    run_case("wide_k36_l70_bias_mean", B=6, L=70, K=36, d=64, Dc=32, C=70, score_type="mean", seed=12,
+             use_bias=True, hist_len=[0, 70, 69, 1, 35, 70])
     return 0
 
 

@@ -60,6 +60,35 @@ def test_supported_shapes(lib):
     assert lib.miner_supported(7, 50, 768, 200, 32) == -1           # bad dtype -> EINVAL
 
 
+def test_wide_path_shapes(lib):
+    """Past the fused kernel (K > 32 or L > 64) the wide path takes K <= 64, L <= 256, Dc <= 256,
+    d <= 768 (include/miner_wide.h); the host routing (ops._fused_or_wide) follows these answers."""
+    F32, BF16 = _lib.DTYPE_F32, _lib.DTYPE_BF16
+    assert lib.miner_wide_supported(F32, 120, 256, 64, 64) == 0
+    assert lib.miner_wide_supported(BF16, 200, 768, 200, 64) == 0       # config-5 user dims
+    assert lib.miner_wide_supported(F32, 257, 256, 64, 32) == -2        # L > 256
+    assert lib.miner_wide_supported(F32, 50, 256, 64, 65) == -2         # K > 64
+    assert lib.miner_wide_supported(F32, 50, 1024, 64, 32) == -2        # d > 768
+    assert lib.miner_wide_supported(BF16, 50, 96, 64, 32) == -2         # 16-bit: d % 64
+    assert lib.miner_wide_supported(F32, 50, 96, 64, 32) == 0
+    assert lib.miner_wide_supported(9, 50, 256, 64, 32) == -1
+    with pytest.raises(ValueError, match="wide path"):
+        ops._fused_or_wide(F32, 300, 256, 64, 32)
+    assert ops._fused_or_wide(F32, 50, 256, 64, 32) is True
+    assert ops._fused_or_wide(F32, 120, 256, 64, 64) is False
+
+
+def test_wide_argument_errors_before_any_launch(lib):
+    P = ctypes.c_void_p(16)
+    assert lib.miner_score_wide(None, 0, 7, P, P, P, None, 0, None, None, 1, 4, 256, 64, P) == -1   # score type
+    assert lib.miner_score_wide(None, 0, 0, P, None, P, None, 0, None, None, 1, 4, 256, 64, P) == -1  # no proj
+    assert lib.miner_score_wide(None, 0, 1, P, None, P, None, 0, None, None, 1, 4, 256, 65, P) == -2  # K > 64
+    assert lib.miner_score_wide(None, 0, 1, P, None, P, None, 0, None, P, 1, 4, 256, 8, P) == -1     # value: weighted
+    assert lib.miner_score_wide(None, 0, 1, P, None, P, None, 0, None, None, 0, 4, 256, 8, P) == 0   # B = 0: no launch
+    assert lib.miner_wide_proj(None, 0, P, P, 4, 96, P) == -2                                       # d % 64
+    assert lib.miner_wide_proj(None, 0, None, P, 4, 128, P) == -1
+
+
 def test_lds_fits_one_cu(lib):
     for dt in (_lib.DTYPE_F32, _lib.DTYPE_BF16):
         for st in (0, 1, 2, 3):

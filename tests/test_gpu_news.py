@@ -15,7 +15,7 @@ import torch
 
 from miner_amd import news, ops, synthetic
 from oracle import miner_oracle as orc
-from tests.conftest import golden_names, load_golden
+from tests.conftest import load_golden, news_golden_names
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -81,7 +81,7 @@ def _ok(x, ref, dtype, what):
 
 
 # ---- parity against the reference's own outputs (fp32) ------------------------------------------
-@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("name", news_golden_names())
 def test_fp32_matches_reference(name):
     g = load_golden(name)
     weighted = g["score_type"] == "weighted"
@@ -95,7 +95,7 @@ def test_fp32_matches_reference(name):
     _ok(mui, g["mui"], torch.float32, f"{name} mui")
 
 
-@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("name", news_golden_names())
 def test_fp32_bf16x6_matches_reference(name, monkeypatch):
     """The optional bf16x6 form of the fp32 kernel (MINER_NEWS_F32X6=1: every fp32 operand cut exactly
     into three bf16 terms, six bf16 MFMAs per contraction) at the same fp32 bar as the default."""

@@ -166,7 +166,7 @@ def test_unsupported_shape_raises():
     M = torch.ones((2, 4), dtype=torch.bool, device=DEV)
     C = torch.zeros((2, 3, 64), device=DEV)
     W1 = torch.zeros((8, 64), device=DEV)
-    Q = torch.zeros((65, 8), device=DEV)   # K = 65 > 32 in this build
+    Q = torch.zeros((65, 8), device=DEV)   # K = 65: past the fused kernel (32) and the wide path (64)
     W2 = torch.zeros((64, 64), device=DEV)
     with pytest.raises(ValueError):
         _ops().score(E, M, C, W1, Q, W2)
