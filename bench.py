@@ -420,6 +420,8 @@ def run_news(args, rank, world, dev):
     s16 = o16[0]
     assert torch.isfinite(s16).all()
     c2 = config2_line(args, rank, world, dev) if not args.no_config2 else None
+    c4 = config4_subline(dev) if (world == 1 and not args.no_config2) else None
+    c5 = config5_subline(dev) if (world == 1 and not args.no_config2) else None
 
     if rank != 0:
         return
@@ -465,7 +467,8 @@ def run_news(args, rank, world, dev):
         "precompute": {"kernel": "news_pre<fp32>", "ms": round(pre32, 4), "flops": pre_fl,
                        "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
                        "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
-        "bf16_mode": bf16_mode, "config2": c2, "metric_step": metric_step, "dense_rows_kernel": dense,
+        "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "metric_step": metric_step,
+        "dense_rows_kernel": dense,
         "cpu_baseline": cpu, "auc_parity": auc,
     }
     print(json.dumps(line), flush=True)
@@ -659,6 +662,77 @@ def corpus_cpu_baseline(seconds: float = 10.0):
                       f"rows in chunks of 4096, fp32, {el:.1f}s (top-k selection not included)"}
 
 
+def _kernel_ms(fn, steps, warmup, dev):
+    """Mean HIP-event time of ``fn()`` on the current stream after ``warmup`` untimed calls."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    st = torch.cuda.current_stream(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(steps):
+        fn()
+    b.record(st)
+    torch.cuda.synchronize(dev)
+    return a.elapsed_time(b) / steps
+
+
+def config4_subline(dev, steps=5, warmup=2):
+    """BASELINE config 4 (FastFormer, 50k impressions, bf16) measured inside the default run, so the
+    driver's bench carries it; the full line is ``--workload fastformer``."""
+    from miner_amd import fastformer as ff
+    from miner_amd import synthetic
+    g = torch.Generator().manual_seed(1000)
+    lens = torch.randint(0, FF_L + 1, (FF_B,), generator=g)
+    mask = (torch.arange(FF_L)[None, :] >= (FF_L - lens)[:, None]).to(dev)
+    hist = (torch.randn(FF_B, FF_L, FF_H, generator=g) * 0.0625).to(dev, torch.bfloat16)
+    cand = (torch.randn(FF_B, FF_C, FF_H, generator=g) * 0.0625).to(dev, torch.bfloat16)
+    pk = ff.pack(synthetic.fastformer_params(0).to(dev), torch.bfloat16)
+    out = [None]
+
+    def fn():
+        out[0] = ff.score(hist, mask, cand, pk)
+
+    ms = _kernel_ms(fn, steps, warmup, dev)
+    assert torch.isfinite(out[0]).all()
+    tflops = ff_flops_per_impression() * FF_B / (ms / 1e3) / 1e12
+    return {"workload": "config 4 FastFormer user encoder (L=50, hidden 256, 16 heads, 2 layers, C=40)",
+            "value": round(FF_B * FF_C / (ms / 1e3), 1), "unit": "pairs/s", "dtype": "bf16",
+            "impressions_per_step": FF_B, "ms_per_step": round(ms, 4), "steps": steps,
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "kernel": "ff_fused<bf16>"}}
+
+
+def config5_subline(dev, steps=2, warmup=1):
+    """BASELINE config 5 (full-corpus ranking: 2048 users x 200k news, L=200, K=64, fp16, top-100) measured
+    inside the default run; the full line is ``--workload corpus``."""
+    from miner_amd import corpus, synthetic
+    dt = torch.float16
+    g = torch.Generator(device=dev).manual_seed(5)
+    table = (torch.randn((C5_N, D), generator=g, device=dev) / D ** 0.5).to(dt)
+    W1, Q, W2 = synthetic.init_weights(5, D, DC, C5_K, device=dev)
+    pk = corpus.pack_encoder(W1, Q, W2, dtype=dt)
+    hid = torch.randint(0, C5_N, (C5_U, C5_L), generator=g, device=dev, dtype=torch.int32)
+    lens = torch.randint(1, C5_L + 1, (C5_U,), generator=g, device=dev)
+    mask = torch.arange(C5_L, device=dev)[None, :] >= (C5_L - lens)[:, None]
+    out = [None]
+
+    def fn():
+        mui, proj = corpus.encode_users(table, mask, pk, his_ids=hid)
+        out[0] = corpus.rank_topk(mui, proj, table, C5_TOPK)
+
+    ms = _kernel_ms(fn, steps, warmup, dev)
+    assert torch.isfinite(out[0][0]).all()
+    fl = C5_U * C5_N * 4 * C5_K * D
+    tflops = fl / (ms / 1e3) / 1e12
+    return {"workload": "config 5 full-corpus ranking (2048 users x 200k news, L=200, K=64, top-100)",
+            "value": round(C5_U * C5_N / (ms / 1e3), 1), "unit": "(user,news) pairs/s", "dtype": "fp16",
+            "ms_per_step": round(ms, 3), "steps": steps,
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / PEAK_BF16_TFLOPS, 4),
+                         "kernel": "ue_fused<fp16> + rk_fused<fp16> (ranker FLOPs over the whole step)"}}
+
+
 def run_corpus(args, rank, world, dev):
     """BASELINE config 5: every user against the whole 200k-news table (fp16), history 200, K=64,
     fused click score + running top-k (never materialising the U x N scores). One step = encode
@@ -829,7 +903,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dense", action="store_true", help="skip the dense-row kernel comparison")
-    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 sub-line")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 / -4 / -5 sub-lines")
     ap.add_argument("--no-metrics", action="store_true", help="skip the device metric step")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--news-traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_news.json"))
