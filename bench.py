@@ -319,6 +319,8 @@ def device_metrics(scores, dev):
     lab[rows, s.argmin(1)] = 0
     offs = torch.arange(0, (s.shape[0] + 1) * C, C, dtype=torch.int32, device=dev)
     names = ["auc", "group_auc", "mrr", "ndcg@5", "ndcg@10", "hit@5", "hit@10"]
+    n_w = min(1000, s.shape[0])         # warm call (library init, first launches) on a slice
+    metrics.compute_metrics(torch.sigmoid(s[:n_w]).reshape(-1), lab[:n_w].reshape(-1), offs[:n_w + 1], names)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     m = metrics.compute_metrics(torch.sigmoid(s).reshape(-1), lab.reshape(-1), offs, names)

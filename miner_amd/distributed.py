@@ -162,7 +162,8 @@ def reduce_device_metrics(probs: torch.Tensor, labels: torch.Tensor, offsets: to
     with the per-impression metrics computed by the GPU kernel (miner_amd.metrics)."""
     from . import metrics as gm
     rank, ws = world()
-    per = gm.per_impression(probs, labels, offsets, [m for m in metrics if m != "auc"])
+    per = gm.per_impression_device(probs, labels, offsets, [m for m in metrics if m != "auc"])
+    sums = gm.nan_sums(per)
     out = {}
     for metric in metrics:
         if metric == "auc":
@@ -173,12 +174,10 @@ def reduce_device_metrics(probs: torch.Tensor, labels: torch.Tensor, offsets: to
             auc = gm.global_auc(sc.to(probs.device), lb.to(probs.device)) if rank == 0 else None
             out["auc"] = broadcast_float(auc)
             continue
-        vals = per[metric]
-        ok = ~np.isnan(vals)
-        s, c = all_reduce_sum(np.array([vals[ok].sum(), ok.sum()], np.float64))
+        s, c = all_reduce_sum(np.array(sums[metric], np.float64))
         out[evaluation.metric_key(metric)] = float(s / c) if c > 0 else float("nan")
         if save_result:
-            full = gather_concat_to_root(torch.from_numpy(vals))
+            full = gather_concat_to_root(per[metric].cpu())
             if rank == 0:
                 full = full.cpu().numpy()
                 w = full.astype(int) if metric.startswith("hit") else full

@@ -27,11 +27,32 @@ def _ks(metrics: Sequence[str]) -> List[int]:
     return sorted({int(m.split("@")[1]) for m in metrics if m.startswith(("ndcg@", "hit@"))})
 
 
-def per_impression(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: Sequence[str]) -> Dict[str, np.ndarray]:
+def _dcg_rows(Y: np.ndarray, S: np.ndarray, k: int) -> np.ndarray:
+    """compute_dcg_score (evaluation.py:195-231) of every row of S / Y at once: np.argsort along the
+    rows sorts each row exactly as the 1-D call does (tests/test_evaluation.py pins this)."""
+    kk = min(Y.shape[1], k)
+    yt = np.take_along_axis(Y, np.argsort(S, axis=1)[:, ::-1][:, :kk], axis=1)
+    gains = 2 ** yt - 1
+    discounts = np.log2(np.arange(kk) + 2)
+    return np.sum(gains / discounts, axis=1)
+
+
+def ndcg_rows(Y: np.ndarray, S: np.ndarray, k: int) -> np.ndarray:
+    return _dcg_rows(Y, S, k) / _dcg_rows(Y, Y, k)
+
+
+def mrr_rows(Y: np.ndarray, S: np.ndarray) -> np.ndarray:
+    """compute_mrr_score (evaluation.py:177-192) of every row at once."""
+    yt = np.take_along_axis(Y, np.argsort(S, axis=1)[:, ::-1], axis=1)
+    return np.sum(yt / (np.arange(Y.shape[1]) + 1), axis=1) / np.sum(yt, axis=1)
+
+
+def per_impression_device(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: Sequence[str]) -> Dict[str, Tensor]:
     """probs [N] (ranked values, fp32), labels [N] (0/1), offsets [G+1] int32 — device tensors.
 
-    Returns {metric: float64 array [G]} for every per-impression metric named in ``metrics``
-    (group_auc, mrr, ndcg@k, hit@k); impression g owns [offsets[g], offsets[g+1]).
+    Returns {metric: float64 device tensor [G]} for every per-impression metric named in ``metrics``
+    (group_auc, mrr, ndcg@k, hit@k); impression g owns [offsets[g], offsets[g+1]). Nothing but the
+    count of mixed-label ties comes back to the host.
     """
     for t in (probs, labels, offsets):
         if t.device.type != "cuda":
@@ -52,21 +73,45 @@ def per_impression(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: Sequ
                                                  probs.data_ptr(), lab.data_ptr(), offs.data_ptr(), G,
                                                  karr, nk, out.data_ptr(), mixed.data_ptr())
     _lib.check(rc, "miner_impression_metrics")
-    res = out.cpu().numpy()
-    mix = np.flatnonzero(mixed.cpu().numpy())
-    if mix.size:   # the reference's argsort order among mixed-label ties: host recompute
-        o = offs.cpu().numpy()
-        for g in mix:
-            p = probs[o[g]:o[g + 1]].double().cpu().numpy()
-            y = lab[o[g]:o[g + 1]].cpu().numpy().astype(np.int64)
-            res[g, 1] = evaluation.compute_mrr_score(y, p)
+    mix = torch.nonzero(mixed).reshape(-1) if G else None
+    if mix is not None and mix.numel():
+        # the reference's argsort order among mixed-label ties (np.argsort, evaluation.py:188, :208):
+        # those rows are recomputed on the host by the reference formulas, batched per candidate count
+        lo, hi = offs[mix].long(), offs[mix + 1].long()
+        lens = (hi - lo).cpu().numpy()
+        for c in np.unique(lens):
+            sel = np.flatnonzero(lens == c)
+            rows = mix[torch.from_numpy(sel).to(mix.device)]
+            idx = lo[torch.from_numpy(sel).to(lo.device)][:, None] + torch.arange(int(c), device=lo.device)
+            P = probs[idx].double().cpu().numpy()
+            Y = lab[idx].cpu().numpy().astype(np.int64)
+            fix = out[rows].cpu().numpy()
+            fix[:, 1] = mrr_rows(Y, P)
             for t, k in enumerate(ks):
-                res[g, 2 + t] = evaluation.compute_ndcg_score(y, p, k)
-    cols = {"group_auc": res[:, 0], "mrr": res[:, 1]}
+                fix[:, 2 + t] = ndcg_rows(Y, P, k)
+            out[rows] = torch.from_numpy(fix).to(out.device)
+    cols = {"group_auc": out[:, 0], "mrr": out[:, 1]}
     for t, k in enumerate(ks):
-        cols[f"ndcg@{k}"] = res[:, 2 + t]
-        cols[f"hit@{k}"] = res[:, 2 + nk + t]
+        cols[f"ndcg@{k}"] = out[:, 2 + t]
+        cols[f"hit@{k}"] = out[:, 2 + nk + t]
     return {m: cols[evaluation.metric_key(m)] for m in metrics if m != "auc"}
+
+
+def per_impression(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: Sequence[str]) -> Dict[str, np.ndarray]:
+    """``per_impression_device`` with the arrays on the host (float64 [G] per metric)."""
+    return {m: v.cpu().numpy() for m, v in per_impression_device(probs, labels, offsets, metrics).items()}
+
+
+def nan_sums(cols: Dict[str, Tensor]) -> Dict[str, tuple]:
+    """{metric: (sum of the non-NaN values, their count)} reduced on the device, one copy back:
+    the pieces of ``np.nanmean`` (evaluation.py:56-82) that add up across ranks."""
+    if not cols:
+        return {}
+    names = list(cols)
+    v = torch.stack([cols[m] for m in names])
+    ok = ~torch.isnan(v)
+    red = torch.stack([torch.where(ok, v, torch.zeros_like(v)).sum(1), ok.sum(1).to(torch.float64)]).cpu().numpy()
+    return {m: (float(red[0, i]), float(red[1, i])) for i, m in enumerate(names)}
 
 
 def global_auc(probs: Tensor, labels: Tensor) -> float:
@@ -98,15 +143,17 @@ def global_auc(probs: Tensor, labels: Tensor) -> float:
 def compute_metrics(probs: Tensor, labels: Tensor, offsets: Tensor, metrics: List[str], save_result: bool = False,
                     path: str = None) -> Dict[str, float]:
     """The reference's metric dict (src/evaluation.py:36-84) for impressions already sorted by id."""
-    per = per_impression(probs, labels, offsets, metrics)
+    per = per_impression_device(probs, labels, offsets, metrics)
+    sums = nan_sums(per)
     out = {}
     for m in metrics:
         if m == "auc":
             out["auc"] = global_auc(probs, labels)
             continue
-        vals = per[m]
-        out[evaluation.metric_key(m)] = float(np.nanmean(vals))
+        s, c = sums[m]
+        out[evaluation.metric_key(m)] = s / c if c > 0 else float("nan")       # np.nanmean
         if save_result:
+            vals = per[m].cpu().numpy()
             w = vals.astype(int) if m.startswith("hit") else vals
             evaluation.save_scores(os.path.join(path, evaluation.metric_file(m)), w.tolist())
     return out

@@ -128,3 +128,21 @@ def test_reference_metric_functions():
     assert ev.compute_ndcg_score(y, s, 3) == pytest.approx(mo.ndcg(y, s, 3))
     assert ev.is_hit(y, s, 1) == mo.hit(y, s, 1) == 1
     assert ev.auc_score(y, s) == pytest.approx(4 / 6)
+
+
+def test_row_batched_tie_order_equals_reference_calls():
+    """miner_amd.metrics recomputes mixed-label ties for many impressions at once (np.argsort along
+    rows); every row must equal the reference formulas called one impression at a time."""
+    from miner_amd import metrics as gm
+    rng = np.random.default_rng(3)
+    for c in (2, 5, 16, 17, 40, 97):
+        S = rng.integers(0, 4, size=(300, c)).astype(np.float64) / 4     # heavy ties
+        Y = rng.integers(0, 2, size=(300, c)).astype(np.int64)
+        Y[:, 0], Y[:, 1] = 1, 0
+        mrr = gm.mrr_rows(Y, S)
+        for k in (5, 10):
+            nd = gm.ndcg_rows(Y, S, k)
+            for r in range(S.shape[0]):
+                assert nd[r] == ev.compute_ndcg_score(Y[r], S[r], k)
+        for r in range(S.shape[0]):
+            assert mrr[r] == ev.compute_mrr_score(Y[r], S[r])
