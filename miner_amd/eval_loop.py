@@ -392,7 +392,9 @@ def main(argv=None):
     loss, scores = run()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    t1 = time.perf_counter()
     preds_path = _write_predictions(path, preds, rank)       # trainer.py:288-289 ("eval" in mode)
+    el_w = time.perf_counter() - t1
     if rank == 0:
         log.info("Model: %s (MI355X, %s%s)", name, args.precision, ", per-candidate category bias" if category else "")
         log.info("Dataset: %s", "synthetic" if args.synthetic else (args.data_name or args.eval_behaviors_path))
@@ -402,8 +404,8 @@ def main(argv=None):
             log.info("Loss %s", loss)
         for m in args.metrics:
             log.info("Metric %s: %s", m, scores[evaluation.metric_key(m)] if scores else None)
-        log.info("Evaluation time %.3f s (%.1f M samples/s); outputs in %s (%s)", el, total / el / 1e6, path,
-                 os.path.basename(preds_path) if preds_path else "-")
+        log.info("Evaluation time %.3f s (%.1f M samples/s); outputs in %s (%s, written in %.2f s)", el,
+                 total / el / 1e6, path, os.path.basename(preds_path) if preds_path else "-", el_w)
     if world > 1:
         torch.distributed.destroy_process_group()
     return loss, scores

@@ -116,11 +116,36 @@ def save_predictions(path: str, probs: torch.Tensor, impression_ids: torch.Tenso
     else:
         sizes = np.diff(cand_offsets.cpu().numpy().astype(np.int64))
     ids = np.repeat(impression_ids.cpu().numpy().astype(np.int64), sizes)
-    pred = {"pred": [[float(x)] for x in p.tolist()], "impression_id": ids.tolist()}
     out = os.path.join(path, "preds.pkl")
     with open(out, "wb") as f:
-        pickle.dump(pred, f)
+        if ids.size and (ids.min() < 0 or ids.max() >= 2 ** 31):
+            pickle.dump({"pred": [[float(x)] for x in p.tolist()], "impression_id": ids.tolist()}, f)
+        else:
+            f.write(preds_pickle(p.numpy(), ids))
     return out
+
+
+def preds_pickle(probs: np.ndarray, ids: np.ndarray) -> bytes:
+    """The pickle stream of {"pred": [[p], ...], "impression_id": [id, ...]} (protocol 2), written
+    with numpy instead of building 2·N Python objects: pickle.load returns exactly the structure
+    SlowEvaluator.save_predictions pickles (evaluation.py:173-175; floats are the fp32 probabilities
+    widened to double, as float() does). ids must lie in [0, 2^31)."""
+    n = probs.size
+    items = np.empty((n, 11), np.uint8)               # ']' 'G' <8-byte big-endian double> 'a'
+    items[:, 0] = ord("]")
+    items[:, 1] = ord("G")
+    items[:, 2:10] = probs.astype(">f8").view(np.uint8).reshape(n, 8)
+    items[:, 10] = ord("a")
+    ints = np.empty((ids.size, 5), np.uint8)          # 'J' <4-byte little-endian int>
+    ints[:, 0] = ord("J")
+    ints[:, 1:] = ids.astype("<i4").view(np.uint8).reshape(ids.size, 4)
+
+    def key(k: str) -> bytes:
+        b = k.encode()
+        return b"X" + len(b).to_bytes(4, "little") + b
+
+    return b"".join([b"\x80\x02}(", key("pred"), b"](", items.tobytes(), b"e", key("impression_id"), b"](",
+                     ints.tobytes(), b"eu."])
 
 
 def load_miner_state_dict(model: torch.nn.Module, path: str, strict: bool = False):

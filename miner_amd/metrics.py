@@ -194,9 +194,13 @@ class DeviceEvaluator:
         offs = torch.zeros(sizes.numel() + 1, dtype=torch.int64, device=sizes.device)
         offs[1:] = torch.cumsum(sizes, 0)
         if not torch.equal(order, torch.arange(order.numel(), device=order.device)):
-            idx = torch.cat([torch.arange(int(offs[i]), int(offs[i + 1]), device=probs.device) for i in order.tolist()])
-            probs, lab, sizes = probs[idx], lab[idx], sizes[order]
+            # impressions re-laid out in id order (evaluation.py:124, :143), one gather on the device
+            starts = offs[:-1][order]
+            sizes = sizes[order]
             offs[1:] = torch.cumsum(sizes, 0)
+            seg = torch.repeat_interleave(torch.arange(sizes.numel(), device=sizes.device), sizes)
+            idx = starts[seg] + torch.arange(seg.numel(), device=seg.device) - offs[:-1][seg]
+            probs, lab = probs[idx], lab[idx]
         return probs, lab, offs.to(torch.int32)
 
     def compute_scores(self, metrics: List[str], save_result: bool = False, path: str = None) -> Dict[str, float]:

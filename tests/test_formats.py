@@ -77,3 +77,18 @@ def test_state_dict_round_trip(tmp_path):
     for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert ka == kb and torch.equal(va, vb)
     assert set(a.state_dict()) == {"poly_attn.linear.weight", "poly_attn.context_codes", "target_aware_attn.linear.weight"}
+
+
+def test_preds_pickle_stream_equals_pickle_dump():
+    """The numpy-built preds.pkl stream loads to exactly what pickle.dump of the reference's structure
+    (SlowEvaluator.save_predictions, evaluation.py:173-175) loads to, including empty input."""
+    import pickle
+    rng = np.random.default_rng(0)
+    for n in (0, 1, 7, 1000):
+        p = rng.random(n).astype(np.float32)
+        p[: min(n, 2)] = [np.float32(0.5), np.float32(1e-38)][: min(n, 2)]
+        ids = rng.integers(0, 2 ** 31 - 1, n).astype(np.int64)
+        got = pickle.loads(formats.preds_pickle(p, ids))
+        want = {"pred": [[float(x)] for x in p.tolist()], "impression_id": ids.tolist()}
+        assert got == want
+        assert all(type(v[0]) is float for v in got["pred"])
