@@ -116,7 +116,13 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
     use_news = scorer == "news" or (scorer == "auto" and news_ok and max_c <= news.MAX_CAND)
     nt = news.precompute(table, packed, with_proj=score_type == "weighted") if use_news else None
     # with the per-candidate bias every candidate is one sample: chunk by samples (mui is [N, K, d])
-    step = chunk if category is None else max(1, chunk // max(_max_candidates(offs, beh.n), 1))
+    mc = max(_max_candidates(offs, beh.n), 1)
+    step = chunk if category is None else max(1, chunk // mc)
+    # one mui buffer for every chunk of the eval loss (the news kernel writes it; 3.2 GB at 32k x 32 x 768);
+    # with the per-candidate bias a chunk holds up to step x mc one-candidate samples
+    rows = min(step, beh.n) if category is None else min(step * mc, int(offs[-1]))
+    mui_buf = torch.empty((max(rows, 1), packed.K, d), device=table.device, dtype=torch.float32) \
+        if (want_loss and use_news) else None
     for s in range(0, beh.n, step):
         e = min(s + step, beh.n)
         o0, o1 = int(offs[s]), int(offs[e])
@@ -131,7 +137,7 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
             s_off = torch.arange(o1 - o0 + 1, device=table.device, dtype=torch.int32)
         if use_news:
             out = news.score(nt, his, msk, cid, score_type=score_type, cand_offsets=s_off, his_bias=bias,
-                             return_user=want_loss, validate=False)
+                             return_user=want_loss, validate=False, user_out=mui_buf)
         else:
             out = ops.score_gather(table, his, msk, cid, packed, score_type=score_type, cand_offsets=s_off,
                                    his_bias=bias, return_user=want_loss, validate=False)

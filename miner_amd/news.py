@@ -97,13 +97,15 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
 
 def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[Tensor] = None, *,
           score_type: str = "weighted", cand_offsets: Optional[Tensor] = None,
-          his_bias: Optional[Tensor] = None, return_user: bool = False, validate: bool = True):
+          his_bias: Optional[Tensor] = None, return_user: bool = False, validate: bool = True,
+          user_out: Optional[Tensor] = None):
     """Miner.forward after the news encoder (model.py:113-138) for impressions given as news ids.
 
     his_ids [B, L] int, his_mask [B, L] bool (True = real click), cand_ids [B, C] (dense) or [N]
     with cand_offsets [B+1] int32 (ragged), his_bias [B, L] fp32 (category bias averaged over the
     candidates, model.py:176) or None. Returns scores ([B, C] / [N] fp32) and, if return_user,
-    mui [B, K, d] fp32. score_type 'none' returns mui only. ``validate`` checks ids / offsets.
+    mui [B, K, d] fp32. score_type 'none' returns mui only. ``validate`` checks ids / offsets;
+    ``user_out`` is an optional caller-owned fp32 [>= B, K, d] buffer for mui.
     """
     st = _lib.SCORE_TYPES.get(score_type)
     if st is None:
@@ -151,7 +153,15 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
         for ids, what in ((hid, "his_ids"), (cid, "cand_ids")):
             if ids is not None and ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= nt.n_news):
                 raise ValueError(f"{what} must index the news table [0, {nt.n_news})")
-    mui = torch.empty((B, K, d), device=dev, dtype=torch.float32) if (return_user or st == _lib.SCORE_NONE) else None
+    mui = None
+    if return_user or st == _lib.SCORE_NONE:
+        if user_out is not None:        # a caller-owned [>= B, K, d] fp32 buffer, reused across calls
+            if user_out.dtype != torch.float32 or user_out.dim() != 3 or user_out.shape[0] < B or \
+                    tuple(user_out.shape[1:]) != (K, d) or not user_out.is_contiguous():
+                raise ValueError(f"user_out must be a contiguous fp32 [>={B},{K},{d}] tensor")
+            mui = user_out[:B]
+        else:
+            mui = torch.empty((B, K, d), device=dev, dtype=torch.float32)
     with torch.cuda.device(dev):
         rc = _lib.lib().miner_score_news(_stream(dev), dt, st, _ptr(nt.table), _ptr(nt.logits), _ptr(nt.proj),
                                          nt.n_news, _ptr(hid), _ptr(mask), _ptr(his_bias), _ptr(cid), _ptr(offs),
