@@ -550,6 +550,12 @@ __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpre
 // row DMAs of one chunk for this wave (saddr form: the chunk's scalar base + a 32-bit per-lane row
 // offset), parts E[his] / proj[his] / Cand at M0 = mE, mE + PART, mE + 2 PART; one statement, M0
 // saved and restored around it
+// The MINER_NEWS_ABL experiment bits news_score32 honours. Production builds compile them out (0):
+// the uniform branches cost 6 % (15.11 -> 14.17 ms per 131k impressions, bit-identical scores,
+// tools/bisect_news.py); diagnostic builds (tools/stage_profile.py, A/B scripts) pass 0x7fffffff.
+#ifndef MINER_NEWS_ABL_MASK
+#define MINER_NEWS_ABL_MASK 0
+#endif
 #ifndef MINER_NEWS_NT
 #define MINER_NEWS_NT 0
 #endif
@@ -1257,6 +1263,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
+  const int abl = p.abl & MINER_NEWS_ABL_MASK;              // experiment bits (MINER_NEWS_ABL)
   const int L = p.L, d = p.d;
   const int nchunk = NCH > 0 ? NCH : d / kF32CW;
   // softmax over the history (model.py:176-181): smode 2 (d >= 128): every wave computes its own A slice
@@ -1265,9 +1272,9 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   // lane either way, and the cooperative form (smode 1, MINER_NEWS_ABL bit 256) adds two LDS round
   // trips and a partial exchange; smode 0 (one pair per item): in-wave + a barrier before the L2 DMA
   const int npair0 = nchunk >> 1;
-  const int smode = (p.abl & 256) && nchunk >= 6 ? 1 : (npair0 >= 2 ? 2 : 0);
+  const int smode = (abl & 256) && nchunk >= 6 ? 1 : (npair0 >= 2 ? 2 : 0);
   const bool coop = smode == 1;
-  const bool split_f = npair0 >= 2 && !(p.abl & 512);    // pass end without a barrier (see the pass end)
+  const bool split_f = npair0 >= 2 && !(abl & 512);    // pass end without a barrier (see the pass end)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const char* tabB = static_cast<const char*>(p.table);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj) : tabB;
@@ -1388,7 +1395,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   // the X waves 4-7 start their products right after the barrier, alone on their SIMDs while the
   // partner waits on the address path. lv bit jj: history rows of block jj live (E, and proj when
   // weighted), bit 2 + jj: its candidate rows live
-  const bool dma8 = (p.abl & 64) != 0;   // experiment: every wave issues one block of each part
+  const bool dma8 = (abl & 64) != 0;   // experiment: every wave issues one block of each part
   auto dma_block = [&](int jj) { return dma8 ? wave : 2 * (wave & 3) + jj; };
   auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC, unsigned& lv) {
     const int lane = threadIdx.x & 63;
@@ -1419,7 +1426,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     }
     lv = __builtin_amdgcn_readfirstlane(lv);
   };
-  const bool abl_nodma = (p.abl & 2) != 0, abl_nocomp = (p.abl & 4) != 0;   // timing ablations (outputs wrong)
+  const bool abl_nodma = (abl & 2) != 0, abl_nocomp = (abl & 4) != 0;   // timing ablations (outputs wrong)
   NS_STAMP_DECL
   auto dma32 = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int ich, int slot) {
     if (abl_nodma || lv == 0) return;
@@ -1544,7 +1551,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
 
   // S7 on waves 4-7 (the X waves, which wait at the barrier otherwise): wave w candidates [16(w-4), +16) of the finished pass, lane (kq, c) interests
   // [8kq, 8kq+8); the 4 lane rows combined by permlanes (model.py:128-136, :213-214)
-  const bool s7lo = (p.abl & 128) != 0;  // experiment: S7 on waves 0-3
+  const bool s7lo = (abl & 128) != 0;  // experiment: S7 on waves 0-3
   auto s7 = [&]() {
     if (s7lo ? wave >= 4 : wave < 4) return;
     const int lane = threadIdx.x & 63;
@@ -1622,7 +1629,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     // (the ablation branch below also shapes the schedule: without it, and with the chains
     // started on an inline-zero accumulator instead, the kernel measured 7 % slower in a clean
     // per-commit A/B, tools/bisect_news.py; one chain per chunk +5 %)
-    if (p.abl & 32) { h00[0] = a0[0]; h10[0] = a1[0]; } else
+    if (abl & 32) { h00[0] = a0[0]; h10[0] = a1[0]; } else
 #pragma unroll
     for (int s = 0; s < NST; s += 2) {
       h00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], aw[s], h00, 0, 0, 0);
@@ -1645,8 +1652,8 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         cf0[q] = *reinterpret_cast<const f32x4v*>(s0 + 2 * Cf::PART + cOff + q * 2048);
         cf1[q] = *reinterpret_cast<const f32x4v*>(s1 + 2 * Cf::PART + cOff + q * 2048);
       }
-      if (WEIGHTED && P == 1 && !(p.abl & 8)) {
-        if (p.abl & 2048) {            // A/B: the Numerical Recipes erfc form
+      if (WEIGHTED && P == 1 && !(abl & 8)) {
+        if (abl & 2048) {            // A/B: the Numerical Recipes erfc form
 #pragma unroll
           for (int e = 0; e < 4; ++e) x0[e] = gelu_erfc_nr(x0[e]);
         } else {
@@ -1654,7 +1661,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           for (int e = 0; e < 4; ++e) x0[e] = gelu_as_f32(x0[e]);
         }
       }
-      if (p.abl & 16) {
+      if (abl & 16) {
 #pragma unroll
         for (int q = 0; q < NT; ++q) acc[q] += cf0[q] * x0 + cf1[q] * x1;
       } else {
@@ -1663,8 +1670,8 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
 #pragma unroll
           for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(cf0[q][e], x0[e], acc[q], 0, 0, 0);
         }
-        if (WEIGHTED && P == 1 && !(p.abl & 8)) {
-          if (p.abl & 2048) {
+        if (WEIGHTED && P == 1 && !(abl & 8)) {
+          if (abl & 2048) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) x1[e] = gelu_erfc_nr(x1[e]);
           } else {
@@ -1699,7 +1706,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         e0[i] = v.x;
         e1[i] = v.y;
       }
-      if (p.abl & 32) {                        // timing ablation: no history product
+      if (abl & 32) {                        // timing ablation: no history product
         h0[0] += e0[0];
         h1[0] += e1[0];
       } else {
@@ -1722,7 +1729,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         x[2 * e] = h0[e];
         x[2 * e + 1] = h1[e];
       }
-      if (WEIGHTED && P == 1 && !(p.abl & 8)) {
+      if (WEIGHTED && P == 1 && !(abl & 8)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = gelu_as_f32(x[i]);
       }
@@ -1734,7 +1741,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         float c[8];
         *reinterpret_cast<float4*>(c) = *reinterpret_cast<const float4*>(cpart + q * 2048 + xcOff[0]);
         *reinterpret_cast<float4*>(c + 4) = *reinterpret_cast<const float4*>(cpart + q * 2048 + xcOff[1]);
-        if (p.abl & 16) acc[q][0] += c[0] + sb.hi[0];   // timing ablation: no candidate product
+        if (abl & 16) acc[q][0] += c[0] + sb.hi[0];   // timing ablation: no candidate product
         else acc[q] = mma_x6(acc[q], split8(c), sb);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1766,7 +1773,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   };
 
   // static priority for the X-path waves 4-7 (the GELU chain, the longer one of each SIMD's pair)
-  if (!(p.abl & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (!(abl & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int npair = nchunk >> 1;
   for (int ci = 0; ci < n_i; ++ci) {
     int c_off, c_cnt;

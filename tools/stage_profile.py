@@ -24,7 +24,7 @@ FF_STAGES = ["E load + LN0", "G12 q,k", "qfs partial", "q softmax", "pq + qks pa
 
 def build(extra=(), out=STAMP_LIB):
     from miner_amd.build import hipcc, SOURCES, ARCH
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMINER_STAMPS",
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMINER_STAMPS", "-DMINER_NEWS_ABL_MASK=0x7fffffff",
            "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"), *extra, *SOURCES, "-o", out]
     subprocess.run(cmd, check=True)
 
