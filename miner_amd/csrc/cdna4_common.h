@@ -249,6 +249,39 @@ __device__ __forceinline__ float gelu_as_f32(float x) {
   return __builtin_fmaf(hx, copysignf(erfz, x), hx);
 }
 
+// gelu_as_f32 on two values at once in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two results per
+// lane per VALU issue). Per pair 14 full-rate VALU + 2 rcp + 2 exp instead of 22 + 4: the fp32 MFMA
+// excludes VALU on its SIMD, so the GELU's issue cycles add to the MFMA time one for one. The
+// 1/sqrt(2) is folded into the denominator's coefficient and the exponent's (tools/gelu_error.py
+// gelu_as_pk: <= 2.2e-7·max(1, |x|) against float64, the accuracy class of gelu_as_f32).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_as_f32x2(f32x2 x) {
+  constexpr float kA = 0.3275911f * 0.70710678118654752440f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(__builtin_fmaf(kA, fabsf(x[0]), 1.0f)),
+                   __builtin_amdgcn_rcpf(__builtin_fmaf(kA, fabsf(x[1]), 1.0f))};
+  // nq = -t·P5(t): the Horner coefficients negated (exact), so erf needs no negation instruction
+  f32x2 nq = __builtin_elementwise_fma((f32x2)(-1.061405429f), t, (f32x2)(1.453152027f));
+  nq = __builtin_elementwise_fma(nq, t, (f32x2)(-1.421413741f));
+  nq = __builtin_elementwise_fma(nq, t, (f32x2)(0.284496736f));
+  nq = __builtin_elementwise_fma(nq, t, (f32x2)(-0.254829592f));
+  nq = nq * t;
+  const f32x2 y = (x * x) * (f32x2)(-0.72134752044448170368f);       // -z²·log2(e), z = |x|/sqrt(2)
+  const f32x2 e = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+  f32x2 erfz = __builtin_elementwise_fma(nq, e, (f32x2)(1.0f));
+  erfz[0] = copysignf(erfz[0], x[0]);
+  erfz[1] = copysignf(erfz[1], x[1]);
+  const f32x2 hx = x * (f32x2)(0.5f);
+  return __builtin_elementwise_fma(hx, erfz, hx);
+}
+template <class V> __device__ __forceinline__ void gelu_as_pairs(V& x, int n) {   // n even, compile-time
+#pragma unroll
+  for (int e = 0; e < n; e += 2) {
+    const f32x2 r = gelu_as_f32x2(f32x2{x[e], x[e + 1]});
+    x[e] = r[0];
+    x[e + 1] = r[1];
+  }
+}
+
 // bf16-mode transcendentals: branch-free, a handful of VALU ops each.  Their error (tanh: a few
 // fp32 ulp of 1; erf: <= 1.5e-7 absolute, Abramowitz & Stegun 7.1.26) is far below the bf16
 // operand rounding of that mode.  The fp32 parity mode uses the libm tanhf / erff / expf.
@@ -266,7 +299,6 @@ __device__ __forceinline__ float gelu_fast(float x) {
 // bf16-mode GELU without transcendentals, two values per packed-fp32 instruction (v_pk_fma_f32):
 // Φ(x) = 0.5 + x·P(x²) on |x| <= 4 (x clamped there), P the degree-7 weighted least-squares fit of
 // 0.5·erf(x/√2)/x: |ΔΦ| <= 5e-5, so |Δgelu(x)| <= 5e-5·|x| — far below bf16 operand rounding.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_poly2(f32x2 x) {
   f32x2 xc;
   xc.x = __builtin_amdgcn_fmed3f(x.x, -4.0f, 4.0f);

@@ -1657,8 +1657,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) x0[e] = gelu_erfc_nr(x0[e]);
         } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) x0[e] = gelu_as_f32(x0[e]);
+          gelu_as_pairs(x0, 4);
         }
       }
       if (abl & 16) {
@@ -1675,8 +1674,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) x1[e] = gelu_erfc_nr(x1[e]);
           } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x1[e] = gelu_as_f32(x1[e]);
+            gelu_as_pairs(x1, 4);
           }
         }
 #pragma unroll
@@ -1730,8 +1728,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         x[2 * e + 1] = h1[e];
       }
       if (WEIGHTED && P == 1 && !(abl & 8)) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = gelu_as_f32(x[i]);
+        gelu_as_pairs(x, 8);
       }
       const Split8 sb = split8(x);
       NS_STAMP(5);

@@ -14,3 +14,8 @@ def test_gelu_erfc_nr_error_bound():
 def test_gelu_as_f32_error_bound():
     """gelu_as_f32 (Abramowitz & Stegun 7.1.26) in the device's operation order: <= 2.5e-7·max(1, |x|)."""
     assert gelu_error.max_error(gelu_error.gelu_as) <= 2.5e-7
+
+
+def test_gelu_as_f32x2_error_bound():
+    """gelu_as_f32x2 (the packed-fp32 form, constants folded): the same <= 2.5e-7·max(1, |x|)."""
+    assert gelu_error.max_error(gelu_error.gelu_as_pk) <= 2.5e-7

@@ -40,6 +40,21 @@ def gelu_as(x):
     return f32(f32(hx * f32(np.copysign(erfz, x))) + hx)
 
 
+def gelu_as_pk(x):
+    """cdna4_common.h gelu_as_f32x2 (the packed-fp32 form of gelu_as_f32): the 1/sqrt(2) folded into
+    the denominator's coefficient and the exponent's, the rest in the same order."""
+    x = f32(x)
+    t = f32(1) / f32(f32(f32(f32(0.3275911) * f32(0.70710678118654752440)) * f32(abs(x))) + f32(1))
+    q = f32(f32(f32(1.061405429) * t) + f32(-1.453152027))
+    for k in (1.421413741, -0.284496736, 0.254829592):
+        q = f32(f32(q * t) + f32(k))
+    q = f32(q * t)
+    e = f32(np.exp2(f32(f32(x * x) * f32(-0.72134752044448170368))))
+    erfz = f32(f32(1) - f32(q * e))
+    hx = f32(x * f32(0.5))
+    return f32(f32(hx * f32(np.copysign(erfz, x))) + hx)
+
+
 def max_error(fn=gelu_nr):
     xs = np.concatenate([np.linspace(-10, 10, 200001), np.logspace(-8, 1, 2000), -np.logspace(-8, 1, 2000)])
     worst = 0.0
@@ -52,3 +67,4 @@ def max_error(fn=gelu_nr):
 if __name__ == "__main__":
     print(f"max |gelu_nr - gelu| / max(1, |x|) = {max_error(gelu_nr):.3e}")
     print(f"max |gelu_as - gelu| / max(1, |x|) = {max_error(gelu_as):.3e}")
+    print(f"max |gelu_as_pk - gelu| / max(1, |x|) = {max_error(gelu_as_pk):.3e}")
