@@ -333,6 +333,35 @@ def device_metrics(scores, dev):
     return lab, offs, m, (sorted(times[1:])[1], times[0])
 
 
+def host_tolist_line(scores, ms_per_step, n_sample=100_000):
+    """SURVEY §8(d) "with and without host .tolist()": the reference's eval hands every batch's
+    sigmoid(logits) to Python as a list (evaluation.py:165 SlowEvaluator.eval_batch). Timed here:
+    sigmoid on the device + the copy of the whole step's scores into pinned host memory (HIP events
+    around both), and list conversion on a bounded sample of them (scaled to the step; it is
+    per-element host work). The build's own evaluator keeps the scores on the device instead."""
+    B, Cc = scores.shape
+    host = torch.empty((B, Cc), dtype=torch.float32, pin_memory=True)
+    st = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for rep in range(2):                                  # first pass warms the copy path
+        a.record(st)
+        host.copy_(torch.sigmoid(scores), non_blocking=True)
+        b.record(st)
+        torch.cuda.synchronize()
+    d2h_ms = a.elapsed_time(b)
+    n = min(n_sample, B)
+    t0 = time.perf_counter()
+    lst = host[:n].reshape(-1).tolist()
+    tolist_ms = (time.perf_counter() - t0) * 1e3 * (B / n)
+    assert len(lst) == n * Cc
+    per_step = ms_per_step + d2h_ms + tolist_ms
+    return {"value": round(B * Cc / (per_step / 1e3), 1), "unit": "pairs/s",
+            "ms_per_step": round(per_step, 2), "d2h_sigmoid_ms": round(d2h_ms, 2),
+            "tolist_ms": round(tolist_ms, 1),
+            "sample": f"sigmoid + pinned D2H copy of the whole step ({B} x {Cc}); .tolist() timed on "
+                      f"{n} impressions and scaled to {B}"}
+
+
 def auc_parity(s32_full, s16_full, batch, table32, W1, Q, W2, dev, n_imp=2048):
     """The metric's "AUC parity vs ref", on a bounded sample of the timed batch (part of the CPU
     baseline leg): scores of the reference CPU path (the oracle: model.py:113-216 as the same torch
@@ -455,6 +484,7 @@ def run_news(args, rank, world, dev):
                  "auc_delta_vs_fp32": metric_step["bf16_delta"]["auc"] if metric_step else None,
                  "note": "bf16 operands, fp32 accumulation: no reference counterpart (the reference evaluates "
                          "in fp32); its metric deltas vs the fp32 headline are in metric_step.bf16_delta"}
+    with_host = host_tolist_line(s32, el32 / args.steps * 1e3) if world == 1 else None
     cpu = cpu_baseline(args.cpu_seconds) if (world == 1 and not args.no_cpu) else None
     auc = auc_parity(s32, s16, pool[0], table32, W1, Q, W2, dev) if (world == 1 and not args.no_cpu) else None
     line = {
@@ -475,7 +505,7 @@ def run_news(args, rank, world, dev):
                        "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
                        "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
         "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "metric_step": metric_step,
-        "dense_rows_kernel": dense,
+        "dense_rows_kernel": dense, "with_host_tolist": with_host,
         "cpu_baseline": cpu, "auc_parity": auc,
     }
     print(json.dumps(line), flush=True)

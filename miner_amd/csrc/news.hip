@@ -1546,12 +1546,6 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   f32x4v acc[4];                               // M / Lg partials of this wave, candidate tiles 0..3
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  // fp32 form, tail pass (<= 8 candidates past the last full 16-row tile): those candidates' partials
-  // over this lane's 4 columns per chunk, packed (even e, odd e); summed over the lane groups at the
-  // pass end
-  f32x2 tacc[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) tacc[c] = f32x2{0.f, 0.f};
   int pend_off = -1, pend_cnt = 0;
   int t = 0;
 
@@ -1618,35 +1612,9 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   // history product, 2 candidate product, 4 mui out. NST history steps (rows 4s + g, s < NST: A = 0
   // past L) and NT candidate tiles are compile-time, so all LDS reads issue before the MFMAs, and the
   // two chunks' chains interleave (one chunk's GELU beside the other's MFMAs).
-  // candidate rows 16 NT + c (c < 8), columns 16 ct + 4 g .. + 3 of this chunk: one ds_read_b128 each
-  // (the 16 lanes of a group read one address: a broadcast); partials (even e, odd e) per candidate
-  auto tail_rows = [&](const char* sl, const f32x4v& x, auto nt_c) {
-    constexpr int NT = decltype(nt_c)::value;
-    const int g = (threadIdx.x & 63) >> 4;
-    const char* cp = sl + 2 * Cf::PART + NT * 16 * 128;
-    const f32x2 xl = f32x2{x[0], x[1]}, xh = f32x2{x[2], x[3]};
-#pragma unroll
-    for (int c0 = 0; c0 < 8; c0 += 4) {       // 4 rows in flight at a time (VGPR budget)
-      f32x4v v[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        v[c] = *reinterpret_cast<const f32x4v*>(cp + (c0 + c) * 128 + (((4 * ct + g) ^ f32swz(16 * NT + c0 + c)) << 4));
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        tacc[c0 + c] = __builtin_elementwise_fma(f32x2{v[c][0], v[c][1]}, xl, tacc[c0 + c]);
-        tacc[c0 + c] = __builtin_elementwise_fma(f32x2{v[c][2], v[c][3]}, xh, tacc[c0 + c]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // TAIL: candidates 16 NT .. 16 NT + 7 on the VALU instead of a 16-row MFMA tile (v_pk_fma_f32, two
-  // results per lane per issue: half the datapath cycles of the padded tile; the fp32 MFMA and the
-  // VALU share the SIMD's datapath, so the saving is real time)
-  auto compute_t = [&](int ci, int cc0, int mode, auto nst_c, auto nt_c, auto tail_c) {
+  auto compute_t = [&](int ci, int cc0, int mode, auto nst_c, auto nt_c) {
     constexpr int NST = decltype(nst_c)::value;
     constexpr int NT = decltype(nt_c)::value;
-    constexpr bool TAIL = decltype(tail_c)::value;
-    auto tail_chunk = [&](const char* sl, const f32x4v& x) { tail_rows(sl, x, nt_c); };
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const char* s0 = smem + (t & (NS - 1)) * Cf::SLOT;
@@ -1701,7 +1669,6 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
 #pragma unroll
           for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(cf0[q][e], x0[e], acc[q], 0, 0, 0);
         }
-        if constexpr (TAIL) tail_chunk(s0, x0);
         if (WEIGHTED && P == 1 && !(abl & 8)) {
           if (abl & 2048) {
 #pragma unroll
@@ -1715,7 +1682,6 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
 #pragma unroll
           for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(cf1[q][e], x1[e], acc[q], 0, 0, 0);
         }
-        if constexpr (TAIL) tail_chunk(s1, x1);
       }
     }
   };
@@ -1779,7 +1745,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     }
   };
   using I4 = std::integral_constant<int, 4>;
-  auto compute = [&](int ci, int cc0, int mode, int ntile, bool tail_pass) {
+  auto compute = [&](int ci, int cc0, int mode, int ntile) {
     if (!(mode & 1) || abl_nocomp) return;
     if constexpr (X6) {
       auto by_nt = [&](auto nkb_c) {
@@ -1792,20 +1758,11 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       else by_nt(std::integral_constant<int, 2>{});
       return;
     }
-    using F = std::false_type;
-    using Tr = std::true_type;
     auto by_nt = [&](auto nst_c) {
-      if (!(mode & 2)) compute_t(ci, cc0, mode, nst_c, I4{}, F{});
-      else if (decltype(nst_c)::value <= 13 && tail_pass) {   // ntile - 1 MFMA tiles + <= 8 candidates on the VALU
-        if constexpr (decltype(nst_c)::value > 13) {}       // (not instantiated past L = 52: VGPR budget)
-        else if (ntile == 4) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 3>{}, Tr{});
-        else if (ntile == 3) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 2>{}, Tr{});
-        else compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 1>{}, Tr{});
-      }
-      else if (ntile >= 4) compute_t(ci, cc0, mode, nst_c, I4{}, F{});
-      else if (ntile == 3) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 3>{}, F{});
-      else if (ntile == 2) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 2>{}, F{});
-      else compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 1>{}, F{});
+      if (!(mode & 2) || ntile >= 4) compute_t(ci, cc0, mode, nst_c, I4{});
+      else if (ntile == 3) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 3>{});
+      else if (ntile == 2) compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 2>{});
+      else compute_t(ci, cc0, mode, nst_c, std::integral_constant<int, 1>{});
     };
     if (nsteps <= 8) by_nt(std::integral_constant<int, 8>{});
     else if (nsteps <= 13) by_nt(std::integral_constant<int, 13>{});
@@ -1822,9 +1779,6 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     for (int cp = 0; cp < cn; ++cp) {
       const int cntp = min(64, c_cnt - 64 * cp);
       const int ntile = (max(cntp, 1) + 15) >> 4;
-      // fp32 form: a last tile holding <= 8 candidates goes to the VALU (needs the barrier-free pass
-      // end, which publishes the tail's partials; ntile >= 2)
-      const bool tail_pass = !X6 && split_f && nsteps <= 13 && ntile >= 2 && cntp - 16 * (ntile - 1) <= 8;
       const bool need_mui = P == 0 && p.mui_out != nullptr && cp == 0;
       const bool need_c = WITH_CAND && path_live;
       const int mode = (k_live && path_live && (need_c || need_mui)) ? (1 | (need_c ? 2 : 0) | (need_mui ? 4 : 0)) : 0;
@@ -1857,8 +1811,6 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int c = 0; c < 8; ++c) tacc[c] = f32x2{0.f, 0.f};
         } else if (smode == 2 && cp == 0 && u == 1) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
           prep_softmax(ci + 2);
@@ -1880,7 +1832,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           dma32(nH, nC, nLv, 1, (t + 3) & (NS - 1));
         }
         NS_STAMP(3);
-        compute(ci, 2 * u, mode, ntile, tail_pass);
+        compute(ci, 2 * u, mode, ntile);
         NS_STAMP(6);
       }
       if (WITH_CAND && split_f) {
@@ -1892,35 +1844,14 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         const int j = lane & 15, g = lane >> 4;
         if (path_live && k_live) {
           float* F = reinterpret_cast<float*>(smem + kOffX) + (P * 2 + ct) * 2048;
-          const int nmt = tail_pass ? ntile - 1 : ntile;       // MFMA tiles
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            if (q < nmt) {
+            if (q < ntile) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const int c = 16 * q + 4 * g + e;
                 F[c * 32 + ((16 * kt + j) ^ ((c >> 1) & 31))] = acc[q][e];
               }
-            }
-          }
-          if (tail_pass) {
-            // tail candidates 16 nmt + c: the lane's two partials, then the 4 lane groups (columns
-            // 4g .. 4g + 3 of each chunk); lane group g stores candidates 2g, 2g + 1
-            float tv[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-              float v = tacc[c][0] + tacc[c][1];
-              v += __shfl_xor(v, 32);
-              v += __shfl_xor(v, 16);
-              tv[c] = v;
-            }
-#pragma unroll
-            for (int u2 = 0; u2 < 2; ++u2) {
-              const int c = 16 * nmt + 2 * g + u2;
-              float v = tv[0];
-#pragma unroll
-              for (int cc = 1; cc < 8; ++cc) v = (2 * g + u2 == cc) ? tv[cc] : v;
-              F[c * 32 + ((16 * kt + j) ^ ((c >> 1) & 31))] = v;
             }
           }
         }
