@@ -21,6 +21,9 @@ VARIANTS = [("full", 0), ("no prio", 1), ("no row DMA", 2), ("no compute", 4), (
             ("no DMA, no compute", 6), ("no DMA, no hist", 34), ("no DMA, no cand", 18),
             ("no DMA, no MFMA", 50), ("x6 full", "x6:0"), ("x6 no compute", "x6:4"), ("x6 no DMA", "x6:2"),
             ("x6 no cand", "x6:16"), ("x6 no hist", "x6:32"), ("x6 no GELU", "x6:8")]
+if os.environ.get("ABLATE_SET") == "s7":         # S7 placement: second pair (4096), mui waves (128)
+    VARIANTS = [("full", 0), ("S7 at pair 1", 4096), ("S7 on waves 0-3", 128), ("S7 pair 1, waves 0-3", 4224),
+                ("no S7 prio", 1), ("S7 pair 1, no prio", 4097)]
 
 
 def build():
