@@ -1999,6 +1999,8 @@ int launch_score(void* stream, const NsParams& prm) {
     const bool x6 = getenv("MINER_NEWS_F32X6") != nullptr;
     if (prm.d == 768) {                // config 3 (MIND-large): the chunk count compile-time
       if (x6) { NEWS_PICK32(true, 24) } else { NEWS_PICK32(false, 24) }
+    } else if (prm.d == 256 && !getenv("MINER_NEWS_NCH_RT")) {   // config 2 (MIND-small)
+      if (x6) { NEWS_PICK32(true, 8) } else { NEWS_PICK32(false, 8) }
     } else {
       if (x6) { NEWS_PICK32(true, 0) } else { NEWS_PICK32(false, 0) }
     }

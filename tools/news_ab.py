@@ -21,7 +21,7 @@ B = int(sys.argv[2]) if len(sys.argv) > 2 else 131072
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 alt = os.environ.get("AB_ALT", "MINER_NEWS_F32V1" if dt == torch.float32 else "MINER_NEWS_CW64")
 altv = os.environ.get("AB_ALT_VALUE", "1")
-n_news, L, C, d, K, Dc = 104000, 50, 40, 768, 32, 200
+n_news, L, C, d, K, Dc = 104000, 50, 40, int(os.environ.get("AB_D", "768")), 32, 200
 g = torch.Generator(device=dev).manual_seed(36)
 table = (torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5).to(dt)
 lens = torch.randint(0, L + 1, (B,), generator=g, device=dev)
