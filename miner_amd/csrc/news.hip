@@ -620,7 +620,7 @@ __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC
   }
 }
 
-template <class T, int ST, bool RAGGED, int PD, int CW>
+template <class T, int ST, bool RAGGED, int PD, int CW, int NCH = 0>   // NCH: chunks per row (0: d / CW at run time)
 __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cf = NCfg<T, CW>;
@@ -639,8 +639,8 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   constexpr bool SWAP = SKIP && NSLAB == 4;
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
-  const int L = p.L, d = p.d;
-  const int nchunk = d / CW;
+  const int L = p.L, d = NCH > 0 ? NCH * CW : p.d;
+  const int nchunk = NCH > 0 ? NCH : d / CW;
   // cooperative softmax one impression ahead (always for 128-column chunks: the host picks them for d >= 512)
   const bool coop = CW == 128 || (nchunk >= PD + 1 && nchunk >= 4);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1969,16 +1969,21 @@ template <class T>
 int launch_score(void* stream, const NsParams& prm) {
   void (*kern)(NsParams) = nullptr;
   const bool rg = prm.cand_off != nullptr;
-#define NEWS_PICK(PDV, CWV)                                                                              \
+#define NEWS_PICK_N(PDV, CWV, NCHV)                                                                      \
   switch (prm.score_type) {                                                                            \
-    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true, PDV, CWV> : news_score<T, MINER_SCORE_WEIGHTED, false, PDV, CWV>; break; \
-    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false, PDV, CWV>; break;                   \
-    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true, PDV, CWV> : news_score<T, MINER_SCORE_MAX, false, PDV, CWV>; break; \
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true, PDV, CWV, NCHV> : news_score<T, MINER_SCORE_WEIGHTED, false, PDV, CWV, NCHV>; break; \
+    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false, PDV, CWV, NCHV>; break;                   \
+    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true, PDV, CWV, NCHV> : news_score<T, MINER_SCORE_MAX, false, PDV, CWV, NCHV>; break; \
   }
+#define NEWS_PICK(PDV, CWV) NEWS_PICK_N(PDV, CWV, 0)
   if constexpr (sizeof(T) == 2) {
     const int nchunk = prm.d >> 6;
+    const bool rt = getenv("MINER_NEWS_NCH_RT") != nullptr;    // A/B: the run-time chunk count
     if (prm.d % 128 == 0 && prm.d >= 512 && !getenv("MINER_NEWS_CW64")) {
-      NEWS_PICK(1, 128)                // 128-column chunks, double-buffered
+      if (prm.d == 768 && !rt) { NEWS_PICK_N(1, 128, 6) }      // config 3: compile-time chunk count
+      else { NEWS_PICK(1, 128) }       // 128-column chunks, double-buffered
+    } else if (prm.d == 256 && !rt) {
+      NEWS_PICK_N(3, 64, 4)            // config 2
     } else if (nchunk >= 3) {
       NEWS_PICK(3, 64)
     } else if (nchunk == 2) {
@@ -2009,6 +2014,7 @@ int launch_score(void* stream, const NsParams& prm) {
     NEWS_PICK(1, 64)
   }
 #undef NEWS_PICK
+#undef NEWS_PICK_N
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kNewsLds);
   if (e != hipSuccess) return (int)e;
   int grid = num_cus();
