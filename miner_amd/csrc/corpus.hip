@@ -20,6 +20,7 @@
 //             workgroup owns whole users: a running top-k per user in LDS, threshold-filtered, so
 //             the U x N scores never leave the CU.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <math.h>
 
@@ -471,15 +472,15 @@ struct RkLds {
   static constexpr int kTotal = kOffCnt + 64;
 };
 
-template <class T, int NKT, int SCORE>
+template <class T, int NKT, int SCORE, int NCH = 0>   // NCH: 128-byte d-chunks per row (0: at run time)
 __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kW = SCORE == MINER_SCORE_WEIGHTED;
   constexpr int NR = kW ? 2 * NKT : NKT;            // row tiles per user: mui (and proj)
   using LD = RkLds<NR>;
   constexpr int kChunkSlabs = sizeof(T) == 2 ? 2 : 1;
-  const int d = p.d, K = p.K, N = p.N;
-  const int nchunk = d * (int)sizeof(T) / kRowB;
+  const int d = NCH > 0 ? NCH * kRowB / (int)sizeof(T) : p.d, K = p.K, N = p.N;
+  const int nchunk = NCH > 0 ? NCH : d * (int)sizeof(T) / kRowB;
   const int nsteps = (N + kNT - 1) / kNT;
   const int ntiles = (p.U + kUT - 1) / kUT;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -704,7 +705,11 @@ int ue_dispatch(void* stream, const UeParams& prm) {
 
 template <class T, int NKT, int S>
 int rk_launch(void* stream, const RkParams& prm) {
-  auto kern = rk_fused<T, NKT, S>;
+  // d = 768 in 16-bit (config 5): the chunk count compile-time (MINER_RK_NCH_RT: the run-time form)
+  void (*kern)(RkParams) = rk_fused<T, NKT, S>;
+  if constexpr (sizeof(T) == 2) {
+    if (prm.d == 768 && !getenv("MINER_RK_NCH_RT")) kern = rk_fused<T, NKT, S, 12>;
+  }
   constexpr int NR = S == MINER_SCORE_WEIGHTED ? 2 * NKT : NKT;
   const int lds = RkLds<NR>::kTotal;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
