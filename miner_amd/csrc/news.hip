@@ -1252,7 +1252,8 @@ __device__ __forceinline__ void vm_wait_n(int n) {      // s_waitcnt vmcnt(n), n
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-template <int ST, bool RAGGED, bool X6, int NCH>         // NCH: 32-column chunks per row (0: d / 32 at run time)
+template <int ST, bool RAGGED, bool X6, int NCH, int SHP = 0>   // NCH: 32-column chunks per row (0: d / 32 at run time);
+// SHP 1: the MIND shape L = 50, K = 32 compile-time (0: at run time)
 __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using T = float;
@@ -1264,7 +1265,8 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int abl = p.abl & MINER_NEWS_ABL_MASK;              // experiment bits (MINER_NEWS_ABL)
-  const int L = p.L, d = p.d;
+  const int L = SHP == 1 ? 50 : p.L, d = p.d;
+  const int KK = SHP == 1 ? 32 : p.K;
   const int nchunk = NCH > 0 ? NCH : d / kF32CW;
   // softmax over the history (model.py:176-181): smode 2 (d >= 128): every wave computes its own A slice
   // (16 interests) at the item's first pair, the next logit rows and softmax coefficients are staged
@@ -1281,7 +1283,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
   const int P = wave >> 2, ct = (wave >> 1) & 1, kt = wave & 1;   // X6: ct = the chunk of the pair
   const int nsteps = (L + 3) >> 2;
-  const bool k_live = 16 * kt < p.K;
+  const bool k_live = 16 * kt < KK;
   const bool path_live = P == 0 || WEIGHTED;
 
   auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
@@ -1327,9 +1329,9 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     if (i >= n_i) return;
     const int lane = threadIdx.x & 63;
     const int row = min(8 * wave + (lane >> 3), L - 1);
-    const int piece = min(lane & 7, (p.K >> 2) - 1);
+    const int piece = min(lane & 7, (KK >> 2) - 1);
     const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
-    dma_b128_c(p.logits + (size_t)id * p.K + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+    dma_b128_c(p.logits + (size_t)id * KK + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
   };
   auto prep_softmax = [&](int i) {
     if (wave != 3 || i >= n_i) return;
@@ -1385,7 +1387,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
         if (mw != -INFINITY) S += part[(w * 32 + k) * 2 + 1] * expf(mw - M);
       }
       float inv = 1.0f / S;
-      if (k >= p.K) inv = 0.f;
+      if (k >= KK) inv = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) reinterpret_cast<float*>(lg + (l0 + j) * 128)[k] = expf(x[j] - M) * inv;
     }
@@ -1510,7 +1512,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     }
     sum = rows4_sum(sum);
     float inv = 1.0f / sum;
-    if (k >= p.K) inv = 0.f;
+    if (k >= KK) inv = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) aw[s] *= inv;
     split_aw();
@@ -1577,12 +1579,12 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     if constexpr (WEIGHTED) {
       float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, lg[j]);
+      for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) mx = fmaxf(mx, lg[j]);
       mx = rows4_max(mx);
       float sm = 0.f, num = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (8 * kq + j < p.K) {
+        if (8 * kq + j < KK) {
           const float pe = expf(lg[j] - mx);
           sm += pe;
           num = __builtin_fmaf(pe, m[j], num);
@@ -1595,13 +1597,13 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       if (p.score_type == MINER_SCORE_MAX) {
         float mx = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, m[j]);
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) mx = fmaxf(mx, m[j]);
         sc = rows4_max(mx);
       } else {
         float sm = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) sm += m[j];
-        sc = rows4_sum(sm) / (float)p.K;
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) sm += m[j];
+        sc = rows4_sum(sm) / (float)KK;
       }
     }
     if (kq == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
@@ -1640,8 +1642,8 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       }
     }
     f32x4v x0 = h00 + h01, x1 = h10 + h11;
-    if ((mode & 4) && 16 * kt + j < p.K) {
-      float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + 16 * kt + j) * d + kF32CW * cc0 + 16 * ct + 4 * g;
+    if ((mode & 4) && 16 * kt + j < KK) {
+      float* dst = p.mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + j) * d + kF32CW * cc0 + 16 * ct + 4 * g;
       *reinterpret_cast<float4*>(dst) = make_float4(x0[0], x0[1], x0[2], x0[3]);
       *reinterpret_cast<float4*>(dst + kF32CW) = make_float4(x1[0], x1[1], x1[2], x1[3]);
     }
@@ -1715,8 +1717,8 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     }
     NS_STAMP(4);
     const int col0 = kF32CW * (cc0 + ct) + 8 * g;          // this lane's columns col0 .. col0 + 7
-    if ((mode & 4) && 16 * kt + j < p.K) {
-      float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + 16 * kt + j) * d + col0;
+    if ((mode & 4) && 16 * kt + j < KK) {
+      float* dst = p.mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + j) * d + col0;
       *reinterpret_cast<float4*>(dst) = make_float4(h0[0], h1[0], h0[1], h1[1]);
       *reinterpret_cast<float4*>(dst + 4) = make_float4(h0[2], h1[2], h0[3], h1[3]);
     }
@@ -1995,21 +1997,24 @@ int launch_score(void* stream, const NsParams& prm) {
     // fp32: news_score32 (16x16x4 fp32 MFMA tiles, 32-column chunks computed in pairs)
     // fp32: news_score32 on the fp32 matrix cores (exact fp32 fma chains); MINER_NEWS_F32X6=1 selects
     // the bf16x6 form (same accuracy class, bf16 matrix cores; measured equal speed at config 3)
-#define NEWS_PICK32(X6V, NCH)                                                                            \
+#define NEWS_PICK32S(X6V, NCH, SHPV)                                                                     \
     switch (prm.score_type) {                                                                            \
-      case MINER_SCORE_WEIGHTED: kern = rg ? news_score32<MINER_SCORE_WEIGHTED, true, X6V, NCH> : news_score32<MINER_SCORE_WEIGHTED, false, X6V, NCH>; break; \
-      case MINER_SCORE_NONE: kern = news_score32<MINER_SCORE_NONE, false, X6V, NCH>; break;               \
-      default: kern = rg ? news_score32<MINER_SCORE_MAX, true, X6V, NCH> : news_score32<MINER_SCORE_MAX, false, X6V, NCH>; break; \
+      case MINER_SCORE_WEIGHTED: kern = rg ? news_score32<MINER_SCORE_WEIGHTED, true, X6V, NCH, SHPV> : news_score32<MINER_SCORE_WEIGHTED, false, X6V, NCH, SHPV>; break; \
+      case MINER_SCORE_NONE: kern = news_score32<MINER_SCORE_NONE, false, X6V, NCH, SHPV>; break;               \
+      default: kern = rg ? news_score32<MINER_SCORE_MAX, true, X6V, NCH, SHPV> : news_score32<MINER_SCORE_MAX, false, X6V, NCH, SHPV>; break; \
     }
+#define NEWS_PICK32(X6V, NCH) NEWS_PICK32S(X6V, NCH, 0)
     const bool x6 = getenv("MINER_NEWS_F32X6") != nullptr;
+    const bool mind = prm.L == 50 && prm.K == 32 && !getenv("MINER_NEWS_SHP_RT");   // MIND: history 50, 32 interests
     if (prm.d == 768) {                // config 3 (MIND-large): the chunk count compile-time
-      if (x6) { NEWS_PICK32(true, 24) } else { NEWS_PICK32(false, 24) }
+      if (x6) { NEWS_PICK32(true, 24) } else if (mind) { NEWS_PICK32S(false, 24, 1) } else { NEWS_PICK32(false, 24) }
     } else if (prm.d == 256 && !getenv("MINER_NEWS_NCH_RT")) {   // config 2 (MIND-small)
       if (x6) { NEWS_PICK32(true, 8) } else { NEWS_PICK32(false, 8) }
     } else {
       if (x6) { NEWS_PICK32(true, 0) } else { NEWS_PICK32(false, 0) }
     }
 #undef NEWS_PICK32
+#undef NEWS_PICK32S
   } else {
     NEWS_PICK(1, 64)
   }
