@@ -620,7 +620,8 @@ __device__ __forceinline__ void dma_chunk(const uint32_t* oH, const uint32_t* oC
   }
 }
 
-template <class T, int ST, bool RAGGED, int PD, int CW, int NCH = 0>   // NCH: chunks per row (0: d / CW at run time)
+template <class T, int ST, bool RAGGED, int PD, int CW, int NCH = 0, int SHP = 0>   // NCH: chunks per row (0: d / CW at
+// run time); SHP 1: the MIND shape L = 50, K = 32 compile-time (0: at run time)
 __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Cf = NCfg<T, CW>;
@@ -639,7 +640,8 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   constexpr bool SWAP = SKIP && NSLAB == 4;
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
-  const int L = p.L, d = NCH > 0 ? NCH * CW : p.d;
+  const int L = SHP == 1 ? 50 : p.L, d = NCH > 0 ? NCH * CW : p.d;
+  const int KK = SHP == 1 ? 32 : p.K;
   const int nchunk = NCH > 0 ? NCH : d / CW;
   // cooperative softmax one impression ahead (always for 128-column chunks: the host picks them for d >= 512)
   const bool coop = CW == 128 || (nchunk >= PD + 1 && nchunk >= 4);
@@ -698,10 +700,10 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     if (i >= n_i) return;
     const int lane = threadIdx.x & 63;
     const int row = min(8 * wave + (lane >> 3), L - 1);
-    const int piece = min(lane & 7, (p.K >> 2) - 1);
+    const int piece = min(lane & 7, (KK >> 2) - 1);
     const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
-    NEWS_CHK(4, p.logits + (size_t)id * p.K + 4 * piece, 16, p.logits, (size_t)p.n_news * p.K * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
-    dma_b128_c(p.logits + (size_t)id * p.K + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+    NEWS_CHK(4, p.logits + (size_t)id * KK + 4 * piece, 16, p.logits, (size_t)p.n_news * KK * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
+    dma_b128_c(p.logits + (size_t)id * KK + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
   };
   // masked-softmax coefficients of impression i (needs its L1): s_l = logit_l * mul_l + add_l with
   // (mul, add) = (1, bias_l) for a click, (0, 1e-30) for a pad slot (model.py:176-180), (0, -inf)
@@ -765,7 +767,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       }
       float inv;
       if constexpr (sizeof(T) == 2) inv = __builtin_amdgcn_rcpf(S); else inv = 1.0f / S;
-      if (k >= p.K) inv = 0.f;
+      if (k >= KK) inv = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float a = nx_exp<T>(x[j] - M) * inv;
@@ -905,7 +907,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     sum = both_sum(sum);
     float inv;
     if constexpr (sizeof(T) == 2) inv = __builtin_amdgcn_rcpf(sum); else inv = 1.0f / sum;
-    if (r >= p.K) inv = 0.f;
+    if (r >= KK) inv = 0.f;
 #pragma unroll
     for (int ls = 0; ls < 2; ++ls) {
       if constexpr (sizeof(T) == 2) {
@@ -978,12 +980,12 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     if constexpr (WEIGHTED) {
       float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, lg[j]);
+      for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) mx = fmaxf(mx, lg[j]);
       mx = rows4_max(mx);
       float s = 0.f, num = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (8 * kq + j < p.K) {
+        if (8 * kq + j < KK) {
           const float pe = nx_exp<T>(lg[j] - mx);
           s += pe;
           num = __builtin_fmaf(pe, m[j], num);
@@ -996,13 +998,13 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       if (p.score_type == MINER_SCORE_MAX) {
         float mx = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) mx = fmaxf(mx, m[j]);
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) mx = fmaxf(mx, m[j]);
         sc = rows4_max(mx);
       } else {
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) if (8 * kq + j < p.K) s += m[j];
-        sc = rows4_sum(s) / (float)p.K;
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) s += m[j];
+        sc = rows4_sum(s) / (float)KK;
       }
     }
     if (kq == 0 && c < pend_cnt) {
@@ -1047,8 +1049,8 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         mma_slab(ax, ef, af[ls]);
       }
       NS_STAMP(4);
-      if ((mode & 4) && r < p.K) {
-        float* dst = p.mui_out + ((size_t)imp_b(ci) * p.K + r) * d + CW * cc + 32 * sl + 16 * h;
+      if ((mode & 4) && r < KK) {
+        float* dst = p.mui_out + ((size_t)imp_b(ci) * KK + r) * d + CW * cc + 32 * sl + 16 * h;
 #pragma unroll
         for (int e = 0; e < 16; e += 4) *reinterpret_cast<float4*>(dst + e) = make_float4(ax[e], ax[e + 1], ax[e + 2], ax[e + 3]);
       }
@@ -1971,21 +1973,24 @@ template <class T>
 int launch_score(void* stream, const NsParams& prm) {
   void (*kern)(NsParams) = nullptr;
   const bool rg = prm.cand_off != nullptr;
-#define NEWS_PICK_N(PDV, CWV, NCHV)                                                                      \
+#define NEWS_PICK_NS(PDV, CWV, NCHV, SHPV)                                                               \
   switch (prm.score_type) {                                                                            \
-    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true, PDV, CWV, NCHV> : news_score<T, MINER_SCORE_WEIGHTED, false, PDV, CWV, NCHV>; break; \
-    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false, PDV, CWV, NCHV>; break;                   \
-    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true, PDV, CWV, NCHV> : news_score<T, MINER_SCORE_MAX, false, PDV, CWV, NCHV>; break; \
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score<T, MINER_SCORE_WEIGHTED, true, PDV, CWV, NCHV, SHPV> : news_score<T, MINER_SCORE_WEIGHTED, false, PDV, CWV, NCHV, SHPV>; break; \
+    case MINER_SCORE_NONE: kern = news_score<T, MINER_SCORE_NONE, false, PDV, CWV, NCHV, SHPV>; break;                   \
+    default: kern = rg ? news_score<T, MINER_SCORE_MAX, true, PDV, CWV, NCHV, SHPV> : news_score<T, MINER_SCORE_MAX, false, PDV, CWV, NCHV, SHPV>; break; \
   }
+#define NEWS_PICK_N(PDV, CWV, NCHV) NEWS_PICK_NS(PDV, CWV, NCHV, 0)
 #define NEWS_PICK(PDV, CWV) NEWS_PICK_N(PDV, CWV, 0)
   if constexpr (sizeof(T) == 2) {
     const int nchunk = prm.d >> 6;
     const bool rt = getenv("MINER_NEWS_NCH_RT") != nullptr;    // A/B: the run-time chunk count
+    const bool mind = prm.L == 50 && prm.K == 32 && !getenv("MINER_NEWS_SHP_RT");   // MIND: history 50, 32 interests
     if (prm.d % 128 == 0 && prm.d >= 512 && !getenv("MINER_NEWS_CW64")) {
-      if (prm.d == 768 && !rt) { NEWS_PICK_N(1, 128, 6) }      // config 3: compile-time chunk count
+      // config 3: compile-time chunk count (the compile-time shape measured 1.1 % slower here)
+      if (prm.d == 768 && !rt) { NEWS_PICK_N(1, 128, 6) }
       else { NEWS_PICK(1, 128) }       // 128-column chunks, double-buffered
-    } else if (prm.d == 256 && !rt) {
-      NEWS_PICK_N(3, 64, 4)            // config 2
+    } else if (prm.d == 256 && !rt) {  // config 2
+      if (mind) { NEWS_PICK_NS(3, 64, 4, 1) } else { NEWS_PICK_N(3, 64, 4) }
     } else if (nchunk >= 3) {
       NEWS_PICK(3, 64)
     } else if (nchunk == 2) {
@@ -2009,7 +2014,7 @@ int launch_score(void* stream, const NsParams& prm) {
     if (prm.d == 768) {                // config 3 (MIND-large): the chunk count compile-time
       if (x6) { NEWS_PICK32(true, 24) } else if (mind) { NEWS_PICK32S(false, 24, 1) } else { NEWS_PICK32(false, 24) }
     } else if (prm.d == 256 && !getenv("MINER_NEWS_NCH_RT")) {   // config 2 (MIND-small)
-      if (x6) { NEWS_PICK32(true, 8) } else { NEWS_PICK32(false, 8) }
+      if (x6) { NEWS_PICK32(true, 8) } else if (mind) { NEWS_PICK32S(false, 8, 1) } else { NEWS_PICK32(false, 8) }
     } else {
       if (x6) { NEWS_PICK32(true, 0) } else { NEWS_PICK32(false, 0) }
     }
@@ -2020,6 +2025,7 @@ int launch_score(void* stream, const NsParams& prm) {
   }
 #undef NEWS_PICK
 #undef NEWS_PICK_N
+#undef NEWS_PICK_NS
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kNewsLds);
   if (e != hipSuccess) return (int)e;
   int grid = num_cus();
