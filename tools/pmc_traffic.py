@@ -64,7 +64,7 @@ def main():
         if args.out == os.path.join(ROOT, "profiles", "pmc_traffic.json"):
             args.out = os.path.join(ROOT, "profiles", "pmc_traffic_news.json")
     if args.news32:
-        KERNEL_TAGS[:] = ["news_score32ILi0ELb0ELb0ELi24E", "news_score32<0, false, false, 24>"]
+        KERNEL_TAGS[:] = ["news_score32ILi0ELb0ELb0ELi24E", "news_score32<0, false, false, 24>", "news_score32<0, false, false, 24,"]
         workload, kernel = "news_L50_K32_d768_C40_N104000_fp32", "news_score<fp32,weighted>"
         if args.out == os.path.join(ROOT, "profiles", "pmc_traffic.json"):
             args.out = os.path.join(ROOT, "profiles", "pmc_traffic_news_fp32.json")
