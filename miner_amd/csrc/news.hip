@@ -1255,7 +1255,8 @@ __device__ __forceinline__ void vm_wait_n(int n) {      // s_waitcnt vmcnt(n), n
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 template <int ST, bool RAGGED, bool X6, int NCH, int SHP = 0>   // NCH: 32-column chunks per row (0: d / 32 at run time);
-// SHP 1: the MIND shape L = 50, K = 32 compile-time (0: at run time)
+// SHP 1: the MIND shape L = 50, K = 32 compile-time (0: at run time); SHP 2: that shape, no category
+// bias and no mui output (plain scoring: the bench, the eval without eval loss)
 __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using T = float;
@@ -1267,8 +1268,10 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
   const int G = gridDim.x;
   const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
   const int abl = p.abl & MINER_NEWS_ABL_MASK;              // experiment bits (MINER_NEWS_ABL)
-  const int L = SHP == 1 ? 50 : p.L, d = p.d;
-  const int KK = SHP == 1 ? 32 : p.K;
+  const int L = SHP >= 1 ? 50 : p.L, d = p.d;
+  const int KK = SHP >= 1 ? 32 : p.K;
+  const float* const bias = SHP == 2 ? nullptr : p.bias;
+  float* const mui_out = SHP == 2 ? nullptr : p.mui_out;
   const int nchunk = NCH > 0 ? NCH : d / kF32CW;
   // softmax over the history (model.py:176-181): smode 2 (d >= 128): every wave computes its own A slice
   // (16 interests) at the item's first pair, the next logit rows and softmax coefficients are staged
@@ -1317,7 +1320,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
       const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
       dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
     } else if (wave == 3) {
-      if (p.bias) dma_b32(p.bias + base, l1 + 512);
+      if (bias) dma_b32(bias + base, l1 + 512);
     } else if (WITH_CAND && wave >= 4) {
       int off, cnt;
       cands(i, off, cnt);
@@ -1344,7 +1347,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     float mul = 0.f, add = -INFINITY;
     if (l < L) {
       mul = keep ? 1.f : 0.f;
-      add = keep ? (p.bias ? l1_bias(smem, i & 3)[l] : 0.f) : 1e-30f;
+      add = keep ? (bias ? l1_bias(smem, i & 3)[l] : 0.f) : 1e-30f;
     }
     float* pr = reinterpret_cast<float*>(smem + kOffPrep + (i & 1) * kPrepB);
     pr[l] = mul;
@@ -1645,7 +1648,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     }
     f32x4v x0 = h00 + h01, x1 = h10 + h11;
     if ((mode & 4) && 16 * kt + j < KK) {
-      float* dst = p.mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + j) * d + kF32CW * cc0 + 16 * ct + 4 * g;
+      float* dst = mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + j) * d + kF32CW * cc0 + 16 * ct + 4 * g;
       *reinterpret_cast<float4*>(dst) = make_float4(x0[0], x0[1], x0[2], x0[3]);
       *reinterpret_cast<float4*>(dst + kF32CW) = make_float4(x1[0], x1[1], x1[2], x1[3]);
     }
@@ -1720,7 +1723,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     NS_STAMP(4);
     const int col0 = kF32CW * (cc0 + ct) + 8 * g;          // this lane's columns col0 .. col0 + 7
     if ((mode & 4) && 16 * kt + j < KK) {
-      float* dst = p.mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + j) * d + col0;
+      float* dst = mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + j) * d + col0;
       *reinterpret_cast<float4*>(dst) = make_float4(h0[0], h1[0], h0[1], h1[1]);
       *reinterpret_cast<float4*>(dst + 4) = make_float4(h0[2], h1[2], h0[3], h1[3]);
     }
@@ -1783,7 +1786,7 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
     for (int cp = 0; cp < cn; ++cp) {
       const int cntp = min(64, c_cnt - 64 * cp);
       const int ntile = (max(cntp, 1) + 15) >> 4;
-      const bool need_mui = P == 0 && p.mui_out != nullptr && cp == 0;
+      const bool need_mui = P == 0 && mui_out != nullptr && cp == 0;
       const bool need_c = WITH_CAND && path_live;
       const int mode = (k_live && path_live && (need_c || need_mui)) ? (1 | (need_c ? 2 : 0) | (need_mui ? 4 : 0)) : 0;
       const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
@@ -2011,8 +2014,12 @@ int launch_score(void* stream, const NsParams& prm) {
 #define NEWS_PICK32(X6V, NCH) NEWS_PICK32S(X6V, NCH, 0)
     const bool x6 = getenv("MINER_NEWS_F32X6") != nullptr;
     const bool mind = prm.L == 50 && prm.K == 32 && !getenv("MINER_NEWS_SHP_RT");   // MIND: history 50, 32 interests
+    const bool plain = !prm.bias && !prm.mui_out && !getenv("MINER_NEWS_PLAIN_RT");  // no bias, no mui output
     if (prm.d == 768) {                // config 3 (MIND-large): the chunk count compile-time
-      if (x6) { NEWS_PICK32(true, 24) } else if (mind) { NEWS_PICK32S(false, 24, 1) } else { NEWS_PICK32(false, 24) }
+      if (x6) { NEWS_PICK32(true, 24) }
+      else if (mind && plain) { NEWS_PICK32S(false, 24, 2) }
+      else if (mind) { NEWS_PICK32S(false, 24, 1) }
+      else { NEWS_PICK32(false, 24) }
     } else if (prm.d == 256 && !getenv("MINER_NEWS_NCH_RT")) {   // config 2 (MIND-small)
       if (x6) { NEWS_PICK32(true, 8) } else if (mind) { NEWS_PICK32S(false, 8, 1) } else { NEWS_PICK32(false, 8) }
     } else {

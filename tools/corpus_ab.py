@@ -1,5 +1,5 @@
 """A/B of the config-5 ranker with the compile-time chunk count (default) against the run-time one
-(MINER_RK_NCH_RT=1), interleaved in one process; top-k outputs compared exactly.
+(AB_ENV, default MINER_RK_NCH_RT=1), interleaved in one process; top-k outputs compared exactly.
 
     python tools/corpus_ab.py [U] [N] [reps]
 """
@@ -13,6 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from miner_amd import corpus, synthetic  # noqa: E402
 
 dev = "cuda:0"
+AB_ENV = os.environ.get("AB_ENV", "MINER_RK_NCH_RT")   # the variant B switch
 U = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 200000
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
@@ -29,9 +30,9 @@ mui, proj = corpus.encode_users(table, mask, pk, his_ids=hid)
 
 def run(rt):
     if rt:
-        os.environ["MINER_RK_NCH_RT"] = "1"
+        os.environ[AB_ENV] = "1"
     else:
-        os.environ.pop("MINER_RK_NCH_RT", None)
+        os.environ.pop(AB_ENV, None)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     out = corpus.rank_topk(mui, proj, table, topk)
