@@ -2021,7 +2021,10 @@ int launch_score(void* stream, const NsParams& prm) {
       else if (mind) { NEWS_PICK32S(false, 24, 1) }
       else { NEWS_PICK32(false, 24) }
     } else if (prm.d == 256 && !getenv("MINER_NEWS_NCH_RT")) {   // config 2 (MIND-small)
-      if (x6) { NEWS_PICK32(true, 8) } else if (mind) { NEWS_PICK32S(false, 8, 1) } else { NEWS_PICK32(false, 8) }
+      if (x6) { NEWS_PICK32(true, 8) }
+      else if (mind && plain) { NEWS_PICK32S(false, 8, 2) }
+      else if (mind) { NEWS_PICK32S(false, 8, 1) }
+      else { NEWS_PICK32(false, 8) }
     } else {
       if (x6) { NEWS_PICK32(true, 0) } else { NEWS_PICK32(false, 0) }
     }
