@@ -408,8 +408,8 @@ __device__ __forceinline__ float s7_score(const float (&lgv)[4], const float (&m
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
 // ---------------------------------------------------------------------------------------------
-template <class T, int MODE, int NS, bool GATHER>
-__global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
+template <class T, int MODE, int NS, bool GATHER, int SHP = 0>   // SHP 1: the MIND model shape compile-time
+__global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50, Dc = 200, K = 32)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kBf16 = sizeof(T) == 2;
   // news-table gather mode (compile-time, so the dense instantiations carry no gather code)
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   // S1 has 4 MFMAs per W1 slab and wave (S5: 6): it needs a deeper ring to cover L2 latency
   constexpr int PF1 = kBf16 ? MINER_PF_S1 : 1;
   // NS > 0: the embedding dim is a compile-time 32*NS and every slab loop fully unrolls
-  const int L = p.L, d = NS ? 32 * NS : p.d, Dc = p.Dc, K = p.K;
+  const int L = SHP ? 50 : p.L, d = NS ? 32 * NS : p.d, Dc = SHP ? 200 : p.Dc, K = SHP ? 32 : p.K;
   const int ns = d >> 5;
   const int nct = n_ctiles(Dc);
   const T* __restrict__ W1p = static_cast<const T*>(p.wp);
@@ -1018,9 +1018,9 @@ int num_cus() {
 
 inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <class T, int MODE, int NS, bool GATHER = false>
+template <class T, int MODE, int NS, bool GATHER = false, int SHP = 0>
 int launch(void* stream, const Params& prm, int lds) {
-  auto kern = miner_fused<T, MODE, NS, GATHER>;
+  auto kern = miner_fused<T, MODE, NS, GATHER, SHP>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   const int per_cu = kLdsMax / lds > 0 ? (kLdsMax / lds > 2 ? 2 : kLdsMax / lds) : 1;
@@ -1041,6 +1041,11 @@ int run(void* stream, int dtype, int mode, Params prm) {
   prm.offAux = c.offAux; prm.eimg = c.eimg;
   const bool gather = prm.his_ids != nullptr;
   if (dtype == MINER_DTYPE_BF16) {
+    // config 3's model (d = 768, history 50, Dc = 200, K = 32), dense rows: the shape compile-time
+    // as well (MINER_SCORE_SHP_RT: the run-time form, for A/B)
+    if (prm.d == 768 && mode == kFull && !gather && prm.L == 50 && prm.Dc == 200 && prm.K == 32 &&
+        !getenv("MINER_SCORE_SHP_RT"))
+      return launch<__bf16, kFull, 24, false, 1>(stream, prm, c.total);
     // bf16 kernels specialised on the embedding dim (d = 32*NS) so the slab loops fully unroll
     switch (prm.d) {
 #define MINER_NS_CASE(ns)                                                                        \
