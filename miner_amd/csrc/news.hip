@@ -1830,9 +1830,6 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           }
         }
         NS_STAMP(2);
-        // the mui waves issue the next pair's row DMAs at priority 2 (above the X waves' 1), so each
-        // SIMD's DMA issue is not held behind its X wave's products (-2 %, tools/news_ablate.py)
-        if (!dma8 && wave < 4) __builtin_amdgcn_s_setprio(2);
         if (u + 1 < npair) {           // the next pair of this item, else the first pair of the next one
           dma32(cH, cC, cLv, 2 * u + 2, (t + 2) & (NS - 1));
           dma32(cH, cC, cLv, 2 * u + 3, (t + 3) & (NS - 1));
@@ -1841,7 +1838,6 @@ __global__ __launch_bounds__(kThreads) void news_score32(NsParams p) {
           dma32(nH, nC, nLv, 0, (t + 2) & (NS - 1));
           dma32(nH, nC, nLv, 1, (t + 3) & (NS - 1));
         }
-        if (!dma8 && wave < 4) __builtin_amdgcn_s_setprio(0);
         NS_STAMP(3);
         compute(ci, 2 * u, mode, ntile);
         NS_STAMP(6);
