@@ -187,6 +187,8 @@ def cpu_baseline(seconds: float = 15.0, d: int = D):
                 break
         per_cand = n_imp * C / el2
     return {"value": round(batched, 1), "unit": "pairs/s", "cores": hi["threads_used"], "kind": "port",
+            "cores_note": "torch threads = the GPU box's host CPU share per GPU (the pool sets OMP_NUM_THREADS=16 "
+                          "per GPU and asks for worker pools sized to it); host_cpus is the whole machine",
             "sample": f"{pairs // C} impressions x {C} candidates (L={L},K={K},d={d},Dc={DC}), fp32, "
                       f"batched 64 impressions/call, {el:.1f}s",
             "host_cpus": hi["host_cpus"], "affinity_cpus": hi["affinity_cpus"], "cpu_model": hi["cpu_model"],
@@ -252,12 +254,13 @@ def load_pmc(path, workload, B):
     return None
 
 
-def measure_news(table, W1, Q, W2, pool, steps, warmup, world, dev):
-    """One dtype of the news path: per step precompute + score over pool[i % len(pool)].
+def measure_news(table, W1, Q, W2, pool, steps, warmup, world, dev, x2=None):
+    """One dtype of the news path: per step precompute + score over pool[i % len(pool)]. fp32 tables:
+    ``x2`` True = the fp16-pair kernel (news_score_x2, default), False = the fp32-MFMA kernel.
     Returns (elapsed s, precompute ms, scoring ms, {pool index: scores of its last step}, NewsTable)."""
     from miner_amd import news, ops
     pw = ops.pack_weights(W1, Q, W2, dtype=table.dtype)      # once per model, outside the timed region
-    nt = news.precompute(table, pw)
+    nt = news.precompute(table, pw, x2=x2)
     tm = EventTimer(dev, 2)
     out = {}
 
@@ -267,10 +270,10 @@ def measure_news(table, W1, Q, W2, pool, steps, warmup, world, dev):
         e = tm.step() if timed else None
         if e:
             e[0].record(tm.stream)
-        nt = news.precompute(table, pw, out=nt)
+        nt = news.precompute(table, pw, out=nt, x2=x2)
         if e:
             e[1].record(tm.stream)
-        out[i % len(pool)] = news.score(nt, hid, mask, cid, validate=False)
+        out[i % len(pool)] = news.score(nt, hid, mask, cid, validate=False, x2=x2)
         if e:
             e[2].record(tm.stream)
 
@@ -278,30 +281,51 @@ def measure_news(table, W1, Q, W2, pool, steps, warmup, world, dev):
     return elapsed, tm.mean_ms(0), tm.mean_ms(1), out, nt
 
 
-def roofline_news(B, kern_ms, elem, d=D, pmc=None, kernel=""):
+NEWS_MODES = {   # mode -> (fp16/bf16/fp32 MFMA products per fp32-equivalent product, dense peak TFLOP/s)
+    "x2": (3, PEAK_BF16_TFLOPS),        # fp32 operands as fp16 pairs: lo·hi + hi·lo + hi·hi on the fp16 MFMA
+    "mfma32": (1, PEAK_F32_TFLOPS),     # exact fp32 fma chains on the fp32 MFMA
+    "bf16": (1, PEAK_BF16_TFLOPS),      # bf16 operands on the bf16 MFMA
+}
+
+
+def roofline_news(B, kern_ms, elem, d=D, pmc=None, kernel="", mode="bf16"):
+    """Roofline of one news-path scoring launch. Two ceilings: HBM (SURVEY §8(d) bytes at 8 TB/s)
+    and MFMA (the kernel's contraction FLOPs x the MFMA products each costs, at the dtype's dense
+    peak); ``bound`` is the lower of the two (the longer ceiling time) and ``frac`` is against it,
+    the other fraction beside it."""
     by = bytes_per_impression(L, d, C, elem) * B
-    gbs = by / (kern_ms / 1e3) / 1e9
     fl = news_kernel_flops(L, K, d, C) * B
-    tf = fl / (kern_ms / 1e3) / 1e12
-    peak_tf = PEAK_F32_TFLOPS if elem == 4 else PEAK_BF16_TFLOPS
+    cost, peak_tf = NEWS_MODES[mode]
+    t = kern_ms / 1e3
+    gbs = by / t / 1e9
+    tf = fl * cost / t / 1e12
+    hbm_ms = by / (PEAK_HBM_GBS * 1e9) * 1e3
+    mfma_ms = fl * cost / (peak_tf * 1e12) * 1e3
     gathered = news_gathered_bytes(L, d, C, K, elem)
-    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(gbs / PEAK_HBM_GBS, 4),
-            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-            "kernel": kernel, "kernel_ms": round(kern_ms, 4), "impressions_per_launch": B,
-            "algorithmic_bytes_per_impression": bytes_per_impression(L, d, C, elem),
-            "algorithmic_bytes_per_launch": by,
-            "mfma": {"flops_per_impression": news_kernel_flops(L, K, d, C), "achieved_tflops": round(tf, 2),
-                     "peak_tflops": peak_tf, "frac": round(tf / peak_tf, 4),
-                     "busy_frac_pmc": pmc.get("mfma_busy_frac") if pmc else None},
-            "gathered_bytes": {"per_impression": gathered, "per_launch": gathered * B,
-                               "achieved_gbs": round(gathered * B / (kern_ms / 1e3) / 1e9, 1)},
-            "note": "achieved/frac: SURVEY §8(d) bytes (L+C)·d·s + L + 4C per impression (weights and the "
-                    "per-news precompute excluded) over the HIP-event launch time; gathered_bytes: what the "
-                    "kernel moves (history rows of the table and of its projection, candidates, logit rows, ids, "
-                    "scores; re-reads served by L2 / the Infinity Cache); traffic: PMC HBM bytes per launch "
-                    "(2·FETCH_SIZE + WRITE_SIZE, gfx950 correction); mfma: the kernel's contraction FLOPs "
-                    "(2·2KLd + 2·2CdK, unpadded) vs the dense peak of the dtype"}
+    hbm = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    mfma = {"flops_per_impression": news_kernel_flops(L, K, d, C), "mfma_products_per_flop": cost,
+            "achieved_tflops": round(tf, 2), "peak_tflops": peak_tf, "frac": round(tf / peak_tf, 4),
+            "busy_frac_pmc": pmc.get("mfma_busy_frac") if pmc else None}
+    if hbm_ms >= mfma_ms:
+        head = {"bound": "hbm", **hbm}
+    else:
+        head = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak_tf, "unit": "TFLOP/s",
+                "frac": round(tf / peak_tf, 4)}
+    head.update({
+        "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+        "kernel": kernel, "kernel_ms": round(kern_ms, 4), "impressions_per_launch": B,
+        "ceiling_ms": {"hbm": round(hbm_ms, 3), "mfma": round(mfma_ms, 3)},
+        "algorithmic_bytes_per_impression": bytes_per_impression(L, d, C, elem),
+        "algorithmic_bytes_per_launch": by, "hbm": hbm, "mfma": mfma,
+        "gathered_bytes": {"per_impression": gathered, "per_launch": gathered * B,
+                           "achieved_gbs": round(gathered * B / t / 1e9, 1)},
+        "note": "bound = the lower of the two ceilings (HBM: SURVEY §8(d) bytes (L+C)·d·s + L + 4C per impression "
+                "at 8 TB/s, weights and the per-news precompute excluded; MFMA: contraction FLOPs 2·2KLd + 2·2CdK "
+                "(unpadded) x MFMA products per FLOP at the dense peak of the MFMA dtype); achieved over the "
+                "HIP-event launch time; gathered_bytes: what the kernel moves (history rows of the table and of "
+                "its projection, candidates, logit rows, ids, scores; re-reads served by L2 / the Infinity Cache); "
+                "traffic: PMC HBM bytes per launch (2·FETCH_SIZE + WRITE_SIZE, gfx950 correction)"})
+    return head
 
 
 def device_metrics(scores, dev):
@@ -411,7 +435,7 @@ def auc_parity(s32_full, s16_full, batch, table32, W1, Q, W2, dev, n_imp=2048):
 
 def config2_line(args, rank, world, dev):
     """BASELINE config 2 (MIND-small shape: 50k impressions, L=50, K=32, d=256, bf16) on the news
-    path, plus its fp32 parity mode; roofline on §8(d) bytes."""
+    path, plus its fp32 form; rooflines with both ceilings, PMC traffic when profiled."""
     from miner_amd import synthetic
     out = {"workload": "config 2 MIND-small shape, news-id input", "impressions_per_gpu_per_step": C2_B,
            "d": C2_D, "news_table": C2_NEWS}
@@ -422,20 +446,27 @@ def config2_line(args, rank, world, dev):
     for name, tab in (("bf16", t32.to(torch.bfloat16)), ("fp32", t32)):
         el, pre_ms, kern_ms, _, _ = measure_news(tab, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
         elem = 2 if name == "bf16" else 4
+        pmc = load_pmc(args.news_traffic_c2 if name == "bf16" else args.news_traffic_c2_32,
+                       f"news_L{L}_K{K}_d{C2_D}_C{C}_N{C2_NEWS}_{name}", C2_B)
+        kern = "news_score<bf16,weighted,4 chunks>" if name == "bf16" else "news_score_x2<weighted,dense,4 chunks>"
         out[name] = {"value": round(C2_B * C * args.steps * world / el, 1), "unit": "pairs/s",
                      "ms_per_step": round(el / args.steps * 1e3, 4), "precompute_ms": round(pre_ms, 4),
-                     "roofline": roofline_news(C2_B, kern_ms, elem, d=C2_D, kernel=f"news_score<{name},weighted>")}
+                     "roofline": roofline_news(C2_B, kern_ms, elem, d=C2_D, pmc=pmc, kernel=kern,
+                                               mode="bf16" if name == "bf16" else "x2")}
     out["value"] = out["bf16"]["value"]
-    out["dtype"] = "bf16 (config 2's dtype); fp32 parity mode beside it"
+    out["dtype"] = "bf16 (config 2's dtype); fp32 beside it"
     return out
 
 
 def run_news(args, rank, world, dev):
     """BASELINE config 3 on the news-id input, fp32 headline: every step recomputes
-    the per-news precompute over the whole table (news_pre) and scores a batch of impressions
-    (news_score)."""
-    from miner_amd import synthetic
-    B = args.batch or NEWS_B
+    the per-news precompute over the whole table (news_pre + the fp16-pair split) and scores this
+    rank's shard of the 3,000,000-impression eval set (news_score_x2). At N > 1 the one set is
+    sharded (BASELINE config 3: "3M impressions ... sharded across 8xMI355X"; no data-path
+    collective); the per-GPU 3M weak-scaling figure rides beside it."""
+    from miner_amd import distributed, synthetic
+    total = args.batch or NEWS_B
+    _, B = distributed.shard_range(total, rank, world)
     g = torch.Generator(device=dev).manual_seed(36)
     table32 = torch.randn((N_NEWS, D), generator=g, device=dev) / D ** 0.5
     W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
@@ -446,25 +477,51 @@ def run_news(args, rank, world, dev):
     # 3.26-3.37 ms (tools/bisect_dense.py, profiles/r02_dense_bisect.txt)
     dense = dense_kernel_line(dev) if (world == 1 and not args.no_dense) else None
 
-    # headline: fp32 (the reference's precision)
-    el32, pre32, kern32, o32, nt32 = measure_news(table32, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
+    # headline: fp32 (the reference's precision) on the fp16 matrix cores (exact-sum fp16 pairs)
+    el32, pre32, kern32, o32, nt32 = measure_news(table32, W1, Q, W2, pool, args.steps, args.warmup, world, dev,
+                                                  x2=True)
     s32 = o32[0]
     assert torch.isfinite(s32).all()
+    # the exact fp32-MFMA kernel (news_score32) on the same batch: the fp32-fma-chain reference form
+    exact = None
+    if world == 1 and not args.no_exact:
+        n_ex = min(args.steps, 5)
+        elx, prex, kernx, ox, _ = measure_news(table32, W1, Q, W2, pool, n_ex, 1, world, dev, x2=False)
+        d_ex = (ox[0].double() - s32.double()).abs().max() / s32.double().pow(2).mean().sqrt()
+        exact = {"kernel": "news_score32<weighted, dense, fp32 MFMA, 24 chunks>", "steps": n_ex,
+                 "value": round(B * C * n_ex / elx, 1), "unit": "pairs/s", "ms_per_step": round(elx / n_ex * 1e3, 4),
+                 "roofline": roofline_news(B, kernx, 4, pmc=load_pmc(args.news_traffic32x, f"news_L{L}_K{K}_d{D}_C{C}_"
+                                                                                         f"N{N_NEWS}_fp32", B),
+                                           kernel="news_score32<weighted, dense, fp32 MFMA, 24 chunks>", mode="mfma32"),
+                 "max_abs_diff_vs_headline_x_rms": float(d_ex)}
+        del ox
     # bf16 throughput mode, same batch and protocol
     table16 = table32.to(torch.bfloat16)
     el16, pre16, kern16, o16, nt16 = measure_news(table16, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
     s16 = o16[0]
     assert torch.isfinite(s16).all()
+    # N > 1: the per-GPU weak-scaling figure (NEWS_B impressions on every rank)
+    weak = None
+    if world > 1 and not args.no_weak:
+        del o16
+        pw_ = [news_batch(5000 + rank, NEWS_B, N_NEWS, dev)]
+        n_w = min(args.steps, 5)
+        elw, _, kernw, _, _ = measure_news(table32, W1, Q, W2, pw_, n_w, 1, world, dev, x2=True)
+        weak = {"scaling": "weak", "impressions_per_gpu_per_step": NEWS_B, "global_batch": NEWS_B * world,
+                "steps": n_w, "value": round(NEWS_B * C * n_w * world / elw, 1), "unit": "pairs/s",
+                "ms_per_step": round(elw / n_w * 1e3, 4), "kernel_ms_rank0": round(kernw, 4)}
+        del pw_
     c2 = config2_line(args, rank, world, dev) if not args.no_config2 else None
     c4 = config4_subline(dev) if (world == 1 and not args.no_config2) else None
     c5 = config5_subline(dev) if (world == 1 and not args.no_config2) else None
 
     if rank != 0:
         return
-    value = B * C * args.steps * world / el32
+    value = total * C * args.steps / el32
     pmc32 = load_pmc(args.news_traffic32, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_fp32", B)
     pmc16 = load_pmc(args.news_traffic, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_bf16", B)
-    roof = roofline_news(B, kern32, 4, pmc=pmc32, kernel="news_score32<weighted, dense, fp32 MFMA, 24 chunks>")
+    roof = roofline_news(B, kern32, 4, pmc=pmc32, mode="x2",
+                         kernel="news_score_x2<weighted, dense, fp16-pair operands, 12 chunks, MIND shape>")
     pre_fl = news_precompute_flops(N_NEWS, D, DC, K)
     # metric step on the device over the whole fp32 batch, and the bf16 AUC delta at full size
     metric_step = None
@@ -474,13 +531,14 @@ def run_news(args, rank, world, dev):
         m16 = metrics.compute_metrics(torch.sigmoid(s16.float()).reshape(-1), lab.reshape(-1), offs, list(m32))
         metric_step = {"ms": round(ms, 2), "ms_first_call": round(ms_first, 2), "pairs": B * C, "impressions": B,
                        "what": "per-impression group_auc/mrr/ndcg@5,10/hit@5,10 kernel + exact global AUC "
-                               "(device radix sort + rank sum) over the whole fp32 batch",
+                               "(device radix sort + rank sum) over rank 0's fp32 batch",
                        "fp32": {k: round(float(v), 6) for k, v in m32.items()},
                        "bf16_delta": {k: float(m16[k] - m32[k]) for k in m32},
                        "cpu_reference": metric_step_cpu_baseline() if (world == 1 and not args.no_cpu) else None}
-    bf16_mode = {"value": round(B * C * args.steps * world / el16, 1), "unit": "pairs/s",
+    bf16_mode = {"value": round(total * C * args.steps / el16, 1), "unit": "pairs/s",
                  "ms_per_step": round(el16 / args.steps * 1e3, 4), "precompute_ms": round(pre16, 4),
-                 "roofline": roofline_news(B, kern16, 2, pmc=pmc16, kernel="news_score<bf16,weighted>"),
+                 "roofline": roofline_news(B, kern16, 2, pmc=pmc16, kernel="news_score<bf16,weighted,6 chunks>",
+                                           mode="bf16"),
                  "auc_delta_vs_fp32": metric_step["bf16_delta"]["auc"] if metric_step else None,
                  "note": "bf16 operands, fp32 accumulation: no reference counterpart (the reference evaluates "
                          "in fp32); its metric deltas vs the fp32 headline are in metric_step.bf16_delta"}
@@ -491,19 +549,25 @@ def run_news(args, rank, world, dev):
         "metric": METRIC,
         "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el32 / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+        "dtype": "fp32",
         "data": "synthetic (seeded MIND-large-shaped impressions as news ids over a random news table; "
                 "random-init weights)",
         "config": {"workload": "config 3 MIND-large shape, news-id input, fp32 (per step: per-news precompute "
-                               "over the whole table + scoring)",
+                               "over the whole table + scoring this rank's shard of the 3M-impression set)",
                    "history": L, "K": K, "d": D, "Dc": DC, "candidates": C, "news_table": N_NEWS,
-                   "impressions_per_gpu_per_step": B, "global_batch": B * world,
+                   "impressions_per_gpu_per_step": B, "global_batch": total,
                    "timed_seconds": round(el32, 3),
-                   "parallelism": f"dp{world} (impression shards, no data-path collective)"},
+                   "parallelism": f"dp{world} (contiguous impression shards of one set, no data-path collective)"},
+        "fp32_arithmetic": "fp32 operands carried as exact-sum fp16 pairs in a power-of-two scale (hi + lo, "
+                           "|x - hi - lo| <= 2^-22 |x|); each fp32 product is lo·hi + hi·lo + hi·hi on the fp16 "
+                           "MFMA with fp32 accumulation; scores within 1e-5 of the reference CPU path "
+                           "(auc_parity; tests/test_gpu_news.py: error vs float64 <= the fp32-MFMA kernel's)",
         "roofline": roof,
-        "precompute": {"kernel": "news_pre<fp32>", "ms": round(pre32, 4), "flops": pre_fl,
-                       "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
+        "precompute": {"kernels": "news_pre<fp32> + x2_absmax/x2_split of the table and of proj", "ms": round(pre32, 4),
+                       "flops": pre_fl, "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
                        "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
+        "fp32_mfma_exact": exact, "weak_scaling": weak,
         "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "metric_step": metric_step,
         "dense_rows_kernel": dense, "with_host_tolist": with_host,
         "cpu_baseline": cpu, "auc_parity": auc,
@@ -894,19 +958,29 @@ def run_dense(args, rank, world, dev):
 # launcher and dry run
 # ---------------------------------------------------------------------------------------------
 def run_dry(args, rank, world, dev):
-    """The launcher + timing protocol without a GPU (gloo): a step is a small CPU matmul."""
+    """The launcher, the config-3 shard plan and the timing protocol without a GPU (gloo): a step is a
+    small CPU matmul; every rank reports its shard of the one 3M-impression set, gathered to rank 0."""
+    from miner_amd import distributed
+    total = args.batch or NEWS_B
+    start, count = distributed.shard_range(total, rank, world)
     a = torch.randn(64, 64)
 
     def step(i, timed):
         torch.mm(a, a)
 
     elapsed = timed_steps(step, args.steps, args.warmup, world, dev)
+    shards = [(start, count)]
+    if world > 1:
+        shards = [None] * world
+        dist.all_gather_object(shards, (start, count))
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(64 * args.steps * world / elapsed, 1), "unit": "pairs/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "dry run (no kernel)",
-                          "config": {"workload": "dry run: launcher and timing protocol only"}}), flush=True)
+                          "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "fp32",
+                          "data": "dry run (no kernel)",
+                          "config": {"workload": "dry run: launcher, shard plan and timing protocol only",
+                                     "global_batch": sum(c for _, c in shards), "shards": shards}}), flush=True)
 
 
 def _free_port():
@@ -944,7 +1018,12 @@ def main():
     ap.add_argument("--no-metrics", action="store_true", help="skip the device metric step")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--news-traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_news.json"))
-    ap.add_argument("--news-traffic32", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_fp32.json"))
+    ap.add_argument("--news-traffic32", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_x2.json"))
+    ap.add_argument("--news-traffic32x", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_fp32.json"))
+    ap.add_argument("--news-traffic-c2", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_c2.json"))
+    ap.add_argument("--news-traffic-c2-32", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_c2_x2.json"))
+    ap.add_argument("--no-exact", action="store_true", help="skip the fp32-MFMA (news_score32) sub-line")
+    ap.add_argument("--no-weak", action="store_true", help="N>1: skip the per-GPU 3M weak-scaling sub-field")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo: launcher and timing protocol only")
     args = ap.parse_args()
     args.steps_set = "--steps" in sys.argv

@@ -73,6 +73,29 @@ int miner_score_news(void* stream, int dtype, int score_type, const void* news_t
                      const int32_t* cand_ids, const int32_t* cand_offsets, int B, int L, int C,
                      int d, int K, float* scores, float* user_out);
 
+/*
+ * fp32 scoring on the fp16 matrix cores (miner_amd/csrc/news_x2.hip; the bench headline since
+ * round 3). Every fp32 operand x is carried as an exact-sum fp16 pair in a power-of-two scale s:
+ * x·s = hi + lo, hi = fp16(x·s), lo = fp16(x·s - hi), |x·s - hi - lo| <= 2^-22·|x·s|; a product
+ * a·b is lo_a·hi_b + hi_a·lo_b + hi_a·hi_b on v_mfma_f32_16x16x32_f16 (fp16 products are exact in
+ * fp32; fp32 accumulation). The pair table takes 4 bytes per element, as fp32.
+ *
+ * miner_news_split_x2: src [n, d] fp32 -> dst [n, d] pairs: per row, per 64-column chunk, the 64
+ *   hi then the 64 lo fp16 values (256 bytes); workspace: miner_news_x2_workspace_floats() floats,
+ *   workspace[0] = s, workspace[1] = 1/s on return (the scale handle miner_score_news_x2 takes).
+ *   Apply it to the news table (the x2 table) and to miner_news_precompute's fp32 news_proj.
+ * miner_score_news_x2: miner_score_news (fp32) from the pair tables: table_scale / proj_scale are
+ *   the workspaces of the two splits (proj2 / proj_scale NULL unless score_type == WEIGHTED).
+ *   Same limits, plus n_news·d·4 < 2^32 (32-bit row offsets).
+ */
+size_t miner_news_x2_workspace_floats(void);
+int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* workspace);
+int miner_score_news_x2(void* stream, int score_type, const void* table2, const float* table_scale,
+                        const float* news_logits, const void* proj2, const float* proj_scale,
+                        int n_news, const int32_t* his_ids, const uint8_t* his_mask,
+                        const float* his_bias, const int32_t* cand_ids, const int32_t* cand_offsets,
+                        int B, int L, int C, int d, int K, float* scores, float* user_out);
+
 /* 0 if (dtype, L, d, Dc, K) is supported by the news path, else the MINER_E* code. Host-only. */
 int miner_news_supported(int dtype, int L, int d, int Dc, int K);
 

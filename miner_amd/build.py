@@ -17,7 +17,8 @@ ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "miner_score.hip")      # the fused scoring kernel
 SOURCES = [SRC, os.path.join(HERE, "csrc", "miner_metrics.hip"), os.path.join(HERE, "csrc", "fastformer.hip"),
            os.path.join(HERE, "csrc", "corpus.hip"), os.path.join(HERE, "csrc", "news.hip"),
-           os.path.join(HERE, "csrc", "miner_auc.hip"), os.path.join(HERE, "csrc", "wide.hip")]
+           os.path.join(HERE, "csrc", "miner_auc.hip"), os.path.join(HERE, "csrc", "wide.hip"),
+           os.path.join(HERE, "csrc", "news_x2.hip")]
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("miner_score.h", "miner_metrics.h", "miner_fastformer.h", "miner_corpus.h", "miner_news.h", "miner_wide.h")] + [os.path.join(HERE, "csrc", "cdna4_common.h")]
 LIB = os.path.join(HERE, "libminer_hip.so")
 ARCH = os.environ.get("MINER_OFFLOAD_ARCH", "gfx950")

@@ -1,0 +1,760 @@
+// news_x2.hip — fp32 MINER scoring from news ids on the fp16 matrix cores (SURVEY.md §8 a1-a7 on
+// the f2 news path), MI355X (gfx950 / CDNA4). The bench headline kernel since round 3.
+//
+// Why. The fp32 scoring kernel news_score32 (news.hip) runs its contractions on the fp32 MFMA:
+// 64 FLOP/clk/SIMD, and it excludes the VALU of its SIMD, so the GELU and every other vector
+// instruction add to the MFMA time (round-2 verdict: MFMA-bound at 0.56 of the fp32 peak). Here
+// every fp32 operand x is carried as an exact-sum pair of fp16 values in a power-of-two scale s,
+//     x·s = hi + lo,  hi = fp16(x·s),  lo = fp16(x·s − hi)          (|x·s − hi − lo| ≤ 2⁻²²·|x·s|)
+// and a product a·b is the three partial products lo_a·hi_b + hi_a·lo_b + hi_a·hi_b on
+// v_mfma_f32_16x16x32_f16 (every fp16 x fp16 product is exact in fp32, the accumulation is fp32;
+// the dropped lo_a·lo_b is below 2⁻²²·|a·b|). The operand error is the fp32 rounding's order, far
+// below the fp32 accumulation error of a 768-long dot product, which both forms share
+// (tests/test_gpu_news_x2.py measures both against float64). Three fp16 MFMAs (48 cycles) replace
+// the 256 cycles of a 16x16x32 contraction on the fp32 MFMA, and they co-issue with the other
+// wave's VALU. The pair planes of the news table and of its projection take 4 bytes per element,
+// the same as fp32, so the gathered bytes do not grow.
+//
+// Kernels:
+//   x2_absmax    per-block max |x| of an fp32 table (partials for the scale)
+//   x2_split     the scale s = 2^(14 − ⌈log2 max|x|⌉) (so |x·s| ≤ 2^14 < 65504) and the pair planes:
+//                row n, 64-column chunk cc: [hi of the 64 columns | lo of the 64 columns], 256 B
+//   news_score_x2  per impression (one persistent workgroup of 8 waves per CU), from the ids:
+//                A   = softmax_L(logits[his] + bias, masked slots = 1e-30)  (model.py:176-181)
+//                mui = A·E[his]                                             (model.py:182)
+//                X   = gelu(A·proj[his]) = gelu(mui·W2ᵀ)                    (model.py:212)
+//                M   = Cand·muiᵀ,  Lg = Cand·Xᵀ                             (model.py:127, :213)
+//                score = Σ_k softmax_k(Lg)·M | max_k M | mean_k M           (model.py:128-136, :214)
+//
+// Stream. The history rows of E and proj and the candidate rows stream in 64-column chunks (one
+// 256-byte row piece per row: both planes) through two 48 KiB LDS slots [E[his] | proj[his] |
+// Cand] (64 rows each), LDS-DMA by id one chunk ahead, one barrier per chunk; rows past L or past
+// the candidate count are not fetched. Wave w = (path P = w >> 2, column half ch = (w >> 1) & 1,
+// interest tile kt = w & 1), so each SIMD pairs a mui wave (P = 0) with an X wave (P = 1, the
+// GELU). Per chunk and wave:
+//   muiᵀ / Xᵀ [32 cols x 16 interests] = part[his]ᵀ·Aᵀ : 2 column tiles x 2 history blocks x 3
+//       MFMAs; the history operand read transposed (ds_read_b64_tr_b16), Aᵀ in registers
+//   M / Lg [16 cands x 16 interests] += Cand·muiᵀ / Xᵀ : 3 MFMAs per candidate tile, the two
+//       accumulators of the first product ARE the B operand (lane (g, i) holds columns 4g..4g+3 of
+//       both column tiles: contraction index 8g + e), split to fp16 pairs in registers
+// At a pass end (<= 64 candidates) each wave publishes its partial M / Lg into its own LDS block;
+// S7 (softmax over K, model.py:213-214) runs on the X waves at the next pass's first chunk.
+// The per-impression ids, mask, bias and logit rows ride in small LDS "aux" blocks DMA'd one to
+// four impressions ahead (as news.hip), so no load the compiler can see is waited on in the loop.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <stdlib.h>
+#include <type_traits>
+
+#include "../../include/miner_news.h"
+#include "cdna4_common.h"
+
+namespace {
+
+constexpr int kThreads = 512;
+constexpr int kWaves = 8;
+constexpr int kMaxL = 64;
+constexpr int kMaxK = 32;
+constexpr int kMaxCand = MINER_NEWS_MAX_CAND;
+constexpr int kCW = 64;                                // columns per chunk
+constexpr int kRB = 256;                               // bytes per staged row piece (hi | lo)
+constexpr int kPart = 64 * kRB;                        // 64 rows: E[his] | proj[his] | Cand
+constexpr int kSlot = 3 * kPart;
+constexpr float kSA = 16384.0f;                        // scale of the attention weights (A <= 1)
+
+// LDS carve (bytes): [ring x2 | F (pass partials) | logit blocks x2 | aux L1 x4 | aux L0 x8 | prep x2]
+constexpr int kRingB = 2 * kSlot;                      // 98304
+constexpr int kFB = 4 * 64 * 32 * 4;                   // F[P][ch] [c][k ^ swz] fp32
+constexpr int kLogB = 64 * 128;                        // 64 history rows x K (<= 32) fp32
+constexpr int kL1B = 4 * 64 * 3 + 4 * kMaxCand;        // his ids | mask words | bias | cand ids
+constexpr int kL0B = 16;
+constexpr int kPrepB = 2 * 64 * 4;                     // softmax (mul | add) per history slot
+constexpr int kOffF = kRingB;
+constexpr int kOffLog = kOffF + kFB;
+constexpr int kOffL1 = kOffLog + 2 * kLogB;
+constexpr int kOffL0 = kOffL1 + 4 * kL1B;
+constexpr int kOffPrep = kOffL0 + 8 * kL0B;
+constexpr int kX2Lds = kOffPrep + 2 * kPrepB;
+static_assert(kX2Lds <= 160 * 1024, "news_score_x2 LDS");
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ float x_both_max(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+__device__ __forceinline__ float x_both_sum(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+// all-reduce over the 4 16-lane rows (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float x_rows4_max(float x) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return x_both_max(fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1])));
+}
+__device__ __forceinline__ float x_rows4_sum(float x) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return x_both_sum(__uint_as_float(s[0]) + __uint_as_float(s[1]));
+}
+
+// one row DMA (saddr form: scalar base + 32-bit per-lane offset) into M0 = m, M0 saved / restored
+__device__ __forceinline__ void x2_dma_row(uint32_t off, const char* base, unsigned m) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(off), "s"(base), "s"(m) : "memory");
+}
+__device__ __forceinline__ void x2_dma_b128(const void* g, unsigned lds) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
+}
+
+// 16-byte chunk swizzle of a staged 256-byte row (16 chunks: hi plane 0..7, lo plane 8..15):
+// chunk slot = chunk ^ x2swz(row). Bits (row bit 2, row bit 0, row bit 1, row bit 3): a bijection
+// on rows 0..15, so the ds_read_b64 candidate operand (16 rows, one chunk, per 32-lane half) is
+// conflict-free; the transposed history reads (rows 8g'..8g'+3 and 8g'+8..8g'+11 of a half, two
+// adjacent chunks) see 8 distinct values of bits 1-3, so their 16 pieces land in 16 chunk slots.
+__host__ __device__ inline int x2swz(int row) { return ((row >> 2) & 1) | ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
+
+__device__ __forceinline__ f32x4 mfma_h(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// c += a·b at fp32 accuracy from fp16 pairs (smallest terms first)
+__device__ __forceinline__ f32x4 mfma_x2(f32x4 c, const u32x4& ah, const u32x4& al, const u32x4& bh, const u32x4& bl) {
+  c = mfma_h(al, bh, c);
+  c = mfma_h(ah, bl, c);
+  return mfma_h(ah, bh, c);
+}
+// two fp32 values -> (hi, lo) fp16 pairs, packed. The residual is taken against the hi bits as
+// packed: left to itself hipcc packs hi with v_cvt_pk_f16_f32 but recomputes the f32 value of hi
+// with a separate v_cvt_f16_f32, and the two round some halfway cases differently (one fp16 ulp of
+// hi lost in 4 of 480k attention weights at config 3; tools/x2_diag.py)
+__device__ __forceinline__ void split2(float x0, float x1, unsigned& hi, unsigned& lo) {
+  const f16x2 h = {(_Float16)x0, (_Float16)x1};
+  unsigned hb = __builtin_bit_cast(unsigned, h);
+  asm volatile("" : "+v"(hb));
+  const f16x2 hh = __builtin_bit_cast(f16x2, hb);
+  const f16x2 l = {(_Float16)(x0 - (float)hh[0]), (_Float16)(x1 - (float)hh[1])};
+  hi = hb;
+  lo = __builtin_bit_cast(unsigned, l);
+}
+// 8 fp32 values -> hi / lo f16x8 operands
+__device__ __forceinline__ void split8h(const float* x, u32x4& hi, u32x4& lo) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    unsigned h, l;
+    split2(x[2 * m], x[2 * m + 1], h, l);
+    hi[m] = h;
+    lo[m] = l;
+  }
+}
+__device__ __forceinline__ uint2 lds_u64(const char* p) { return *reinterpret_cast<const uint2*>(p); }
+__device__ __forceinline__ uint2 lds_tr(const char* p) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds_char*)p));
+}
+
+// ================================================================================================
+// pair planes
+// ================================================================================================
+constexpr int kAbsBlocks = 256;
+
+__global__ __launch_bounds__(256) void x2_absmax(const float* __restrict__ src, size_t n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float m = 0.f;
+  const size_t n4 = n >> 2;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    const float4 v = s4[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  for (size_t i = (n4 << 2) + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) m = fmaxf(m, fabsf(src[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// the scale from the partials: a power of two with max|x|·s <= 2^14 (1 for an all-zero or
+// non-finite table; an infinite or NaN entry then stays one in its pair)
+__device__ __forceinline__ float x2_scale(const float* part, int np) {
+  float m = 0.f;
+  for (int i = 0; i < np; ++i) m = fmaxf(m, part[i]);
+  if (!(m > 0.f) || !isfinite(m)) return 1.0f;
+  int e;
+  frexpf(m, &e);                                     // m = f·2^e, f in [0.5, 1)
+  return ldexpf(1.0f, min(max(14 - e, -126), 127));
+}
+
+// dst row n: for each 64-column chunk, 64 hi then 64 lo fp16 (the x2 layout); scale_out = {s, 1/s}
+__global__ __launch_bounds__(256) void x2_split(const float* __restrict__ src, int N, int d, const float* __restrict__ part,
+                                                unsigned short* __restrict__ dst, float* __restrict__ scale_out) {
+  __shared__ float sc;
+  if (threadIdx.x == 0) sc = x2_scale(part, kAbsBlocks);
+  __syncthreads();
+  const float s = sc;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    scale_out[0] = s;
+    scale_out[1] = 1.0f / s;
+  }
+  const int g8 = d >> 3;                             // groups of 8 columns per row
+  const size_t total = (size_t)N * g8;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t n = i / g8;
+    const int c0 = (int)(i - n * g8) * 8;
+    const float4* p = reinterpret_cast<const float4*>(src + n * d + c0);
+    const float4 a = p[0], b = p[1];
+    const float x[8] = {a.x * s, a.y * s, a.z * s, a.w * s, b.x * s, b.y * s, b.z * s, b.w * s};
+    u32x4 hi, lo;
+    split8h(x, hi, lo);
+    unsigned short* row = dst + n * (size_t)(2 * d) + (c0 >> 6) * 128 + (c0 & 63);
+    *reinterpret_cast<u32x4*>(row) = hi;
+    *reinterpret_cast<u32x4*>(row + 64) = lo;
+  }
+}
+
+// ================================================================================================
+// per-impression scoring
+// ================================================================================================
+struct X2Params {
+  const void* table2;      // [n_news, d] pairs (x2 layout), scale sc_t
+  const float* logits;     // [n_news, K]
+  const void* proj2;       // [n_news, d] pairs, scale sc_p (weighted only)
+  const float* sc_t;       // {s, 1/s}
+  const float* sc_p;
+  const int32_t* his_ids;
+  const uint8_t* mask;
+  const float* bias;
+  const int32_t* cand_ids;
+  const int32_t* cand_off;
+  float* scores;
+  float* mui_out;
+  int n_news, B, L, C, d, K, score_type;
+};
+
+__device__ __forceinline__ int* l1_his(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B); }
+__device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return reinterpret_cast<uint32_t*>(smem + kOffL1 + slot * kL1B + 256); }
+__device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + kOffL1 + slot * kL1B + 512); }
+__device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B + 768); }
+__device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL0 + slot * kL0B); }
+
+// NCH: 64-column chunks per row (0: d / 64 at run time). SHP 2: the MIND shape (history L = 50,
+// K = 32 interests) compile-time, no category bias and no mui output (plain scoring: the bench, the
+// eval without the eval loss); SHP 0: run-time L, K.
+template <int ST, bool RAGGED, int NCH, int SHP>
+__global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
+  constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
+  const int G = gridDim.x;
+  const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;      // impressions of this workgroup
+  const int L = SHP == 2 ? 50 : p.L;
+  const int KK = SHP == 2 ? 32 : p.K;
+  const int d = NCH > 0 ? NCH * kCW : p.d;
+  const int nchunk = NCH > 0 ? NCH : d / kCW;
+  const float* const bias = SHP == 2 ? nullptr : p.bias;
+  float* const mui_out = SHP == 2 ? nullptr : p.mui_out;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int P = wave >> 2, ch = (wave >> 1) & 1, kt = wave & 1;
+  const bool k_live = 16 * kt < KK;
+  const bool path_live = P == 0 || WEIGHTED;
+  const char* tabB = static_cast<const char*>(p.table2);
+  const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj2) : tabB;
+  const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
+  // scales: the history product accumulates s_A·s_part·(A·part)
+  const float iE = p.sc_t[1];
+  const float sPj = WEIGHTED ? p.sc_p[0] : 1.0f, iPj = WEIGHTED ? p.sc_p[1] : 1.0f;
+  const float op_scale = P == 0 ? 1.0f / kSA : (1.0f / kSA) * iPj;   // acc -> s_E·mui | x
+  const float mui_scale = (1.0f / kSA) * iE;                          // acc -> mui
+  const float m_scale = iE * iE, lg_scale = iE * iPj;                 // S7: M_s, Lg_s -> M, Lg
+
+  auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
+  auto cands = [&](int i, int& off, int& cnt) {
+    if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
+    if constexpr (RAGGED) {
+      const int* o = l0_off(smem, i & 7);
+      off = __builtin_amdgcn_readfirstlane(o[0]);
+      cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
+    } else {
+      off = imp_b(i) * p.C;
+      cnt = p.C;
+    }
+    cnt = min(max(cnt, 0), kMaxCand);
+  };
+  // ---- aux DMA jobs (after a barrier): L0 CSR offsets -> L1 ids / mask / bias -> L2 logit rows ----
+  auto issue_L0 = [&](int i) {
+    if (RAGGED && wave == 0 && i < n_i && (threadIdx.x & 63) < 2)
+      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kOffL0 + (i & 7) * kL0B);
+  };
+  auto issue_L1 = [&](int i) {
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const size_t base = (size_t)imp_b(i) * L + min(lane, L - 1);
+    const unsigned l1 = sbase + kOffL1 + (i & 3) * kL1B;
+    if (wave == 1) {
+      dma_b32(p.his_ids + base, l1);
+    } else if (wave == 2) {
+      // the aligned word holding mask byte `base` (the reader picks the byte by address)
+      const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
+      dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
+    } else if (wave == 3) {
+      if (bias) dma_b32(bias + base, l1 + 512);
+    } else if (WITH_CAND && wave >= 4) {                 // candidate ids, 64 per DMA
+      int off, cnt;
+      cands(i, off, cnt);
+      for (int j = wave - 4; j >= 0 && 64 * j < cnt; j += 4) {
+        const int c = min(64 * j + lane, cnt - 1);
+        dma_b32(p.cand_ids + off + c, l1 + 768 + 256 * j);
+      }
+    }
+  };
+  auto issue_L2 = [&](int i) {
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int row = min(8 * wave + (lane >> 3), L - 1);
+    const int piece = min(lane & 7, (KK >> 2) - 1);
+    const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
+    x2_dma_b128(p.logits + (size_t)id * KK + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+  };
+  // masked-softmax coefficients: s_l = logit_l·mul_l + add_l with (1, bias_l) for a click, (0, 1e-30)
+  // for a pad slot (model.py:176-180), (0, -inf) past L
+  auto prep_softmax = [&](int i) {
+    if (wave != 3 || i >= n_i) return;
+    const int l = threadIdx.x & 63;
+    const uint32_t mw = l1_mask(smem, i & 3)[l];
+    const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + l) & 3);
+    const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
+    float mul = 0.f, add = -INFINITY;
+    if (l < L) {
+      mul = keep ? 1.f : 0.f;
+      add = keep ? (bias ? l1_bias(smem, i & 3)[l] : 0.f) : 1e-30f;
+    }
+    float* pr = reinterpret_cast<float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    pr[l] = mul;
+    pr[64 + l] = add;
+  };
+  // row DMAs of a chunk: wave w issues the 4-row blocks w and 8 + (w ^ 4) of every part (the rows
+  // 32..47, live for L = 50 / C = 40, go to the X waves, the mostly-padding rows 48..63 to the mui
+  // waves). Lane l fills row 4b + (l >> 4), chunk slot l & 15 from source chunk slot ^ x2swz(row).
+  // lv bit jj: history rows of block jj live; bit 2 + jj: its candidate rows live.
+  auto dma_block = [&](int jj) { return jj ? 8 + (wave ^ 4) : wave; };
+  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC, unsigned& lv) {
+    const int lane = threadIdx.x & 63;
+    const bool live = i < n_i;
+    int off = 0, cnt = 1;
+    if (live) cands(i, off, cnt);
+    const int cntp = max(1, min(64, cnt - 64 * pass));
+    lv = 0;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row0 = 4 * dma_block(jj);
+      if (live && row0 < L) lv |= 1u << jj;
+      if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 4u << jj;
+      const int row = row0 + (lane >> 4);
+      const uint32_t poff = (uint32_t)(((lane & 15) ^ x2swz(row)) << 4);
+      int h = 0, c = 0;
+      if (live) {
+        h = l1_his(smem, i & 3)[min(row, L - 1)];
+        if (WITH_CAND) c = l1_cand(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
+      }
+      h = min(max(h, 0), p.n_news - 1);
+      c = min(max(c, 0), p.n_news - 1);
+      const uint32_t rowBytes = (uint32_t)d * 4u;
+      oH[jj] = (uint32_t)h * rowBytes + poff;
+      oC[jj] = (uint32_t)c * rowBytes + poff;
+    }
+    lv = __builtin_amdgcn_readfirstlane(lv);
+  };
+  auto dma_chunk = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int cc, int slot) {
+    if (lv == 0) return;
+    const char* bE = tabB + cc * kRB;
+    const char* bP = prjB + cc * kRB;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const unsigned m = sbase + slot * kSlot + dma_block(jj) * 1024;
+      if (lv & (1u << jj)) {
+        x2_dma_row(oH[jj], bE, m);
+        if constexpr (WEIGHTED) x2_dma_row(oH[jj], bP, m + kPart);
+      }
+      if (lv & (4u << jj)) x2_dma_row(oC[jj], bE, m + 2 * kPart);
+    }
+  };
+
+  // ---- per-lane LDS read offsets (fixed for the launch) ----
+  // transposed history reads: lane 4q + p of group g supplies row 8g + 4r + q (read r = 0, 1; + 32 kb
+  // rows = 8192 B by immediate), columns 4p .. 4p + 3 of column tile 2ch + ctl; lane i of the group
+  // receives column i of the 4 rows. Candidate reads: row i (+ 16 ct rows = 4096 B), columns
+  // 32 ch + 16 ctl + 4g .. + 3 (8 B).
+  uint32_t trH[2][2], trL[2][2], cfH[2], cfL[2];
+  {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, i = lane & 15;
+#pragma unroll
+    for (int ctl = 0; ctl < 2; ++ctl) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int row = 8 * g + 4 * rr + q;
+        const int chunk = 4 * ch + 2 * ctl + (pp >> 1);
+        trH[ctl][rr] = row * kRB + ((chunk ^ x2swz(row)) << 4) + 8 * (pp & 1);
+        trL[ctl][rr] = row * kRB + (((chunk + 8) ^ x2swz(row)) << 4) + 8 * (pp & 1);
+      }
+      const int chunk = 4 * ch + 2 * ctl + (g >> 1);
+      cfH[ctl] = i * kRB + ((chunk ^ x2swz(i)) << 4) + 8 * (g & 1);
+      cfL[ctl] = i * kRB + (((chunk + 8) ^ x2swz(i)) << 4) + 8 * (g & 1);
+    }
+  }
+
+  // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kt + i][32 kb + 8g + e]
+  u32x4 aH[2], aL[2];
+  // softmax over the history (model.py:176-181) of this wave's 16 interests, in registers: lane (g, i)
+  // takes the 16 history slots 32 kb + 8g + e, the 4 lane rows combined by permlanes
+  auto softmax_inwave = [&](int i) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const int k = 16 * kt + j;
+    const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
+    const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    float v[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int l = 32 * (s >> 3) + 8 * g + (s & 7);
+      v[s] = __builtin_fmaf(lgb[l * 32 + k], pr[l], pr[64 + l]);
+      mx = fmaxf(mx, v[s]);
+    }
+    mx = x_rows4_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      v[s] = expf(v[s] - mx);                // exp(-inf) = 0 past L
+      sum += v[s];
+    }
+    sum = x_rows4_sum(sum);
+    float inv = kSA / sum;
+    if (k >= KK) inv = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) v[s] *= inv;
+    split8h(v, aH[0], aL[0]);
+    split8h(v + 8, aH[1], aL[1]);
+  };
+
+  // ring rows no DMA writes read as zeros; the prologue's first barrier orders these stores first
+  for (int o = (int)threadIdx.x * 16; o < kRingB; o += kThreads * 16)
+    *reinterpret_cast<u32x4*>(smem + o) = u32x4{0u, 0u, 0u, 0u};
+  for (int i = 0; i < 4; ++i) issue_L0(i);
+  vm_wait_all();
+  raw_barrier();
+  issue_L1(0); issue_L1(1); issue_L1(2);
+  vm_wait_all();
+  raw_barrier();
+  issue_L2(0); issue_L2(1);
+  prep_softmax(0); prep_softmax(1);
+  vm_wait_all();
+  raw_barrier();
+  uint32_t cH[2], cC[2], nH[2] = {0u, 0u}, nC[2] = {0u, 0u};
+  unsigned cLv = 0, nLv = 0;
+  item_offsets(0, 0, cH, cC, cLv);
+  dma_chunk(cH, cC, cLv, 0, 0);
+
+  f32x4 acc[4];                                  // this wave's M / Lg partials, candidate tiles 0..3
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int pend_off = -1, pend_cnt = 0;
+  int t = 0;
+
+  // S7 (model.py:128-136, :213-214) on the X waves 4-7: wave w candidates [16 (w - 4), +16) of the
+  // finished pass, lane (kq, c) interests [8 kq, 8 kq + 8); the two column-half partials summed
+  // here (ch 0 + ch 1), the 4 lane rows combined by permlanes
+  auto s7 = [&]() {
+    if (wave < 4) return;
+    const int lane = threadIdx.x & 63;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int c = 16 * (wave & 3) + cl;
+    const float* F = reinterpret_cast<const float*>(smem + kOffF);
+    const int sw = (c >> 1) & 31;
+    float lg[8], m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = c * 32 + ((8 * kq + j) ^ sw);
+      m[j] = (F[o] + F[2048 + o]) * m_scale;
+      if constexpr (WEIGHTED) lg[j] = (F[4096 + o] + F[6144 + o]) * lg_scale;
+    }
+    float sc;
+    if constexpr (WEIGHTED) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) mx = fmaxf(mx, lg[j]);
+      mx = x_rows4_max(mx);
+      float sm = 0.f, num = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (8 * kq + j < KK) {
+          const float pe = expf(lg[j] - mx);
+          sm += pe;
+          num = __builtin_fmaf(pe, m[j], num);
+        }
+      }
+      sm = x_rows4_sum(sm);
+      num = x_rows4_sum(num);
+      sc = num / sm;
+    } else {
+      if (p.score_type == MINER_SCORE_MAX) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) mx = fmaxf(mx, m[j]);
+        sc = x_rows4_max(mx);
+      } else {
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (8 * kq + j < KK) sm += m[j];
+        sc = x_rows4_sum(sm) / (float)KK;
+      }
+    }
+    if (kq == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
+  };
+
+  // the products of one chunk in slot t & 1; mode: 1 history product, 2 candidate product, 4 mui out;
+  // NT candidate tiles compile-time
+  auto compute_t = [&](int ci, int cc, int mode, auto nt_c) {
+    constexpr int NT = decltype(nt_c)::value;
+    FRESH_LANE_IDS();
+    const int g = lane >> 4, i = lane & 15;
+    const char* slot = smem + (t & 1) * kSlot;
+    const char* part = slot + P * kPart;
+    f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      u32x4 eH[2], eL[2];
+#pragma unroll
+      for (int ctl = 0; ctl < 2; ++ctl) {
+        const uint2 h0 = lds_tr(part + trH[ctl][0] + 8192 * kb), h1 = lds_tr(part + trH[ctl][1] + 8192 * kb);
+        const uint2 l0 = lds_tr(part + trL[ctl][0] + 8192 * kb), l1 = lds_tr(part + trL[ctl][1] + 8192 * kb);
+        eH[ctl] = u32x4{h0.x, h0.y, h1.x, h1.y};
+        eL[ctl] = u32x4{l0.x, l0.y, l1.x, l1.y};
+      }
+#pragma unroll
+      for (int ctl = 0; ctl < 2; ++ctl) hx[ctl] = mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
+    }
+    if ((mode & 4) && 16 * kt + i < KK) {
+      float* dst = mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + i) * d + kCW * cc + 32 * ch + 4 * g;
+#pragma unroll
+      for (int ctl = 0; ctl < 2; ++ctl)
+        *reinterpret_cast<float4*>(dst + 16 * ctl) =
+            make_float4(hx[ctl][0] * mui_scale, hx[ctl][1] * mui_scale, hx[ctl][2] * mui_scale, hx[ctl][3] * mui_scale);
+    }
+    if (mode & 2) {
+      const char* cpart = slot + 2 * kPart;
+      uint2 cH_[NT][2], cL_[NT][2];
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+#pragma unroll
+        for (int ctl = 0; ctl < 2; ++ctl) {
+          cH_[q][ctl] = lds_u64(cpart + cfH[ctl] + 4096 * q);
+          cL_[q][ctl] = lds_u64(cpart + cfL[ctl] + 4096 * q);
+        }
+      }
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] = hx[0][e] * op_scale;
+        x[4 + e] = hx[1][e] * op_scale;
+      }
+      if (WEIGHTED && P == 1) {
+        gelu_as_pairs(x, 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] *= sPj;
+      }
+      u32x4 bH, bL;
+      split8h(x, bH, bL);
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const u32x4 ah = u32x4{cH_[q][0].x, cH_[q][0].y, cH_[q][1].x, cH_[q][1].y};
+        const u32x4 al = u32x4{cL_[q][0].x, cL_[q][0].y, cL_[q][1].x, cL_[q][1].y};
+        acc[q] = mfma_x2(acc[q], ah, al, bH, bL);
+      }
+    }
+  };
+  using I4 = std::integral_constant<int, 4>;
+  auto compute = [&](int ci, int cc, int mode, int ntile) {
+    if (!(mode & 1)) return;
+    if (!(mode & 2) || ntile >= 4) compute_t(ci, cc, mode, I4{});
+    else if (ntile == 3) compute_t(ci, cc, mode, std::integral_constant<int, 3>{});
+    else if (ntile == 2) compute_t(ci, cc, mode, std::integral_constant<int, 2>{});
+    else compute_t(ci, cc, mode, std::integral_constant<int, 1>{});
+  };
+
+  // static priority for the X waves 4-7 (the GELU chain)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  for (int ci = 0; ci < n_i; ++ci) {
+    int c_off, c_cnt;
+    cands(ci, c_off, c_cnt);
+    const int cn = max(1, (c_cnt + 63) >> 6);
+    for (int cp = 0; cp < cn; ++cp) {
+      const int cntp = min(64, c_cnt - 64 * cp);
+      const int ntile = (max(cntp, 1) + 15) >> 4;
+      const bool need_mui = P == 0 && mui_out != nullptr && cp == 0;
+      const bool need_c = WITH_CAND && path_live;
+      const int mode = (k_live && path_live && (need_c || need_mui)) ? (1 | (need_c ? 2 : 0) | (need_mui ? 4 : 0)) : 0;
+      const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
+      bool did_s7 = false;
+      for (int cc = 0; cc < nchunk; ++cc, ++t) {
+        vm_wait_all();                 // this chunk's rows (and every older DMA) landed for this wave,
+        raw_barrier();                 // then for every wave; the other slot is free
+        if (cc == 0) {
+          did_s7 = WITH_CAND && pend_off >= 0;
+          if (did_s7) s7();
+          pend_off = -1;
+          if (cp == 0) {
+            softmax_inwave(ci);
+            if (nchunk == 1) {
+              raw_barrier();           // every wave has read impression ci's logit rows and coefficients
+              issue_L2(ci + 2);
+              prep_softmax(ci + 2);
+            }
+            issue_L0(ci + 4);
+            issue_L1(ci + 3);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else if (cc == 1 && cp == 0) {
+          issue_L2(ci + 2);            // into the block impression ci's logits were read from
+          prep_softmax(ci + 2);
+        }
+        if (cc + 1 < nchunk) {
+          dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
+        } else {
+          item_offsets(ni, np, nH, nC, nLv);
+          dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
+        }
+        compute(ci, cc, mode, ntile);
+      }
+      if constexpr (WITH_CAND) {
+        // pass done: every wave publishes its partial M / Lg [c][k ^ swizzle] into its own block
+        // F[P][ch] without a barrier; S7, after the next chunk's barrier, reads them. The next
+        // publish is at least one barrier after that S7 (one extra barrier when a pass is one chunk).
+        if (nchunk == 1 && did_s7) raw_barrier();
+        const int lane = threadIdx.x & 63;
+        const int j = lane & 15, g = lane >> 4;
+        if (path_live && k_live) {
+          float* F = reinterpret_cast<float*>(smem + kOffF) + (P * 2 + ch) * 2048;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (q < ntile) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int c = 16 * q + 4 * g + e;
+                F[c * 32 + ((16 * kt + j) ^ ((c >> 1) & 31))] = acc[q][e];
+              }
+            }
+          }
+        }
+      }
+      pend_off = c_off + 64 * cp;
+      pend_cnt = cntp;
+      cH[0] = nH[0]; cH[1] = nH[1]; cC[0] = nC[0]; cC[1] = nC[1]; cLv = nLv;
+    }
+  }
+  vm_wait_all();
+  raw_barrier();
+  if (WITH_CAND && pend_off >= 0) s7();
+}
+
+// ================================================================================================
+// host side
+// ================================================================================================
+int x2_num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+
+inline bool al16(const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; }
+
+int x2_launch(void* stream, const X2Params& prm) {
+  void (*kern)(X2Params) = nullptr;
+  const bool rg = prm.cand_off != nullptr;
+#define X2_PICK(NCHV)                                                                                        \
+  switch (prm.score_type) {                                                                                  \
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, NCHV, 0> : news_score_x2<MINER_SCORE_WEIGHTED, false, NCHV, 0>; break; \
+    case MINER_SCORE_NONE: kern = news_score_x2<MINER_SCORE_NONE, false, NCHV, 0>; break;                     \
+    default: kern = rg ? news_score_x2<MINER_SCORE_MAX, true, NCHV, 0> : news_score_x2<MINER_SCORE_MAX, false, NCHV, 0>; break; \
+  }
+  const bool plain = prm.L == 50 && prm.K == 32 && !prm.bias && !prm.mui_out && prm.score_type == MINER_SCORE_WEIGHTED &&
+                     !getenv("MINER_NEWS_SHP_RT");
+  if (prm.d == 768) {                  // config 3 (MIND-large): the chunk count compile-time
+    if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 12, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2>;
+    else { X2_PICK(12) }
+  } else if (prm.d == 256) {           // config 2 (MIND-small)
+    if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 4, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2>;
+    else { X2_PICK(4) }
+  } else {
+    X2_PICK(0)
+  }
+#undef X2_PICK
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kX2Lds);
+  if (e != hipSuccess) return (int)e;
+  int grid = x2_num_cus();
+  if (grid > prm.B) grid = prm.B;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), kX2Lds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t miner_news_x2_workspace_floats(void) { return (size_t)kAbsBlocks + 8; }
+
+int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* workspace) {
+  if (!src || !dst || !workspace || n <= 0 || d <= 0) return MINER_EINVAL;
+  if (d % 64) return MINER_ESHAPE;
+  if (!al16(src) || !al16(dst) || !al16(workspace)) return MINER_EALIGN;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(x2_absmax, dim3(kAbsBlocks), dim3(256), 0, s, src, (size_t)n * d, workspace + 8);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const size_t groups = (size_t)n * (d >> 3);
+  const int grid = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
+  hipLaunchKernelGGL(x2_split, dim3(grid), dim3(256), 0, s, src, n, d, workspace + 8, static_cast<unsigned short*>(dst),
+                     workspace);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+int miner_score_news_x2(void* stream, int score_type, const void* table2, const float* table_scale,
+                        const float* news_logits, const void* proj2, const float* proj_scale, int n_news,
+                        const int32_t* his_ids, const uint8_t* his_mask, const float* his_bias,
+                        const int32_t* cand_ids, const int32_t* cand_offsets, int B, int L, int C, int d, int K,
+                        float* scores, float* user_out) {
+  if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
+  if (!table2 || !table_scale || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
+  if (L <= 0 || d <= 0 || K <= 0) return MINER_EINVAL;
+  if (L > kMaxL || K > kMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
+  if ((uint64_t)n_news * (uint64_t)d * 4u > 0xffffffffull) return MINER_ESHAPE;   // 32-bit row offsets
+  if (score_type == MINER_SCORE_WEIGHTED && (!proj2 || !proj_scale)) return MINER_EINVAL;
+  if (score_type != MINER_SCORE_NONE) {
+    if (!scores || !cand_ids) return MINER_EINVAL;
+    if (!cand_offsets && (C < 0 || C > kMaxCand)) return MINER_ESHAPE;
+  } else if (!user_out) {
+    return MINER_EINVAL;
+  }
+  if (!al16(table2) || !al16(news_logits) || !al16(proj2)) return MINER_EALIGN;
+  if (B == 0) return MINER_OK;
+  X2Params prm{table2, news_logits, proj2, table_scale, proj_scale ? proj_scale : table_scale, his_ids, his_mask, his_bias,
+               score_type == MINER_SCORE_NONE ? nullptr : cand_ids,
+               score_type == MINER_SCORE_NONE ? nullptr : cand_offsets,
+               scores, user_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type};
+  return x2_launch(stream, prm);
+}
+
+}  // extern "C"

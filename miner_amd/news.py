@@ -19,6 +19,7 @@ Device tensors only: there is no CPU path. float32 is the parity mode, bfloat16 
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Optional
 
 import torch
@@ -32,12 +33,23 @@ MAX_CAND = 512          # MINER_NEWS_MAX_CAND: candidates per impression
 
 
 @dataclasses.dataclass
+class PairPlanes:
+    """fp32 tables as exact-sum fp16 pairs (miner_news_split_x2): the operands of the fp32 scoring
+    kernel on the fp16 matrix cores (news_x2.hip). Same bytes as fp32; ``*_ws`` hold the scale."""
+    table2: Tensor                # [n_news, 2d] fp16 (per 64-column chunk: 64 hi | 64 lo)
+    table_ws: Tensor              # fp32 workspace, [0] = scale, [1] = 1/scale
+    proj2: Optional[Tensor]
+    proj_ws: Optional[Tensor]
+
+
+@dataclasses.dataclass
 class NewsTable:
     """A news-embedding table with its per-news precompute (miner_news_precompute output)."""
     table: Tensor                 # [n_news, d] dtype
     logits: Tensor                # [n_news, K] fp32
     proj: Optional[Tensor]        # [n_news, d] dtype, None when built without w_target
     K: int
+    x2: Optional[PairPlanes] = None   # fp32 tables only: the pair planes of table and proj
 
     @property
     def dtype(self) -> torch.dtype:
@@ -63,12 +75,38 @@ def _check_shape(dt: int, L: int, d: int, Dc: int, K: int) -> None:
                          "(L <= 64, K <= 32 and K % 4 == 0, d % 64 == 0)")
 
 
+def x2_enabled() -> bool:
+    """fp32 scoring on the fp16 matrix cores (news_x2.hip) unless MINER_NEWS_FP32=mfma32 selects the
+    fp32-MFMA kernel news_score32 (A/B and the exact-fp32 sub-line of the bench)."""
+    return os.environ.get("MINER_NEWS_FP32", "x2") != "mfma32"
+
+
+def split_x2(src: Tensor, out: Optional[Tensor] = None, ws: Optional[Tensor] = None):
+    """fp32 [n, d] -> (pairs [n, 2d] fp16, workspace with the scale) (miner_news_split_x2)."""
+    _require_device(src)
+    src = _contig(src)
+    if src.dtype != torch.float32 or src.dim() != 2:
+        raise ValueError("split_x2 takes an fp32 [n, d] table")
+    n, d = src.shape
+    if out is None or tuple(out.shape) != (n, 2 * d):
+        out = torch.empty((n, 2 * d), device=src.device, dtype=torch.float16)
+    nws = int(_lib.lib().miner_news_x2_workspace_floats())
+    if ws is None or ws.numel() < nws:
+        ws = torch.empty((nws,), device=src.device, dtype=torch.float32)
+    with torch.cuda.device(src.device):
+        rc = _lib.lib().miner_news_split_x2(_stream(src.device), _ptr(src), n, d, _ptr(out), _ptr(ws))
+    _lib.check(rc, "miner_news_split_x2")
+    return out, ws
+
+
 def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = None,
                w_target: Optional[Tensor] = None, *, with_proj: bool = True,
-               out: Optional[NewsTable] = None) -> NewsTable:
+               out: Optional[NewsTable] = None, x2: Optional[bool] = None) -> NewsTable:
     """logits = tanh(E·W1ᵀ)·Qᵀ [n_news, K] fp32 and proj = E·W2ᵀ [n_news, d] for a news table
     (model.py:171-174, :212). ``w_poly`` is a PackedWeights or the raw weights
-    (w_poly [Dc,d], context_codes [K,Dc], w_target [d,d]); ``out`` reuses its buffers."""
+    (w_poly [Dc,d], context_codes [K,Dc], w_target [d,d]); ``out`` reuses its buffers.
+    fp32 tables also get their fp16 pair planes (``x2``, default: x2_enabled()), the operands of
+    the fp32 scoring kernel on the fp16 matrix cores."""
     _require_device(news_table, context_codes, w_target)
     if not isinstance(w_poly, PackedWeights):
         _require_device(w_poly)
@@ -92,20 +130,28 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
         rc = _lib.lib().miner_news_precompute(_stream(table.device), dt, _ptr(table), n_news, _ptr(pw.buf), d,
                                               pw.Dc, pw.K, _ptr(logits), _ptr(proj))
     _lib.check(rc, "miner_news_precompute")
-    return NewsTable(table, logits, proj, pw.K)
+    planes = None
+    if dtype == torch.float32 and (x2_enabled() if x2 is None else x2):
+        o = out.x2 if out is not None and out.x2 is not None else None
+        t2, tws = split_x2(table, None if o is None else o.table2, None if o is None else o.table_ws)
+        p2, pws = (split_x2(proj, None if o is None else o.proj2, None if o is None else o.proj_ws)
+                   if proj is not None else (None, None))
+        planes = PairPlanes(t2, tws, p2, pws)
+    return NewsTable(table, logits, proj, pw.K, planes)
 
 
 def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[Tensor] = None, *,
           score_type: str = "weighted", cand_offsets: Optional[Tensor] = None,
           his_bias: Optional[Tensor] = None, return_user: bool = False, validate: bool = True,
-          user_out: Optional[Tensor] = None):
+          user_out: Optional[Tensor] = None, x2: Optional[bool] = None):
     """Miner.forward after the news encoder (model.py:113-138) for impressions given as news ids.
 
     his_ids [B, L] int, his_mask [B, L] bool (True = real click), cand_ids [B, C] (dense) or [N]
     with cand_offsets [B+1] int32 (ragged), his_bias [B, L] fp32 (category bias averaged over the
     candidates, model.py:176) or None. Returns scores ([B, C] / [N] fp32) and, if return_user,
     mui [B, K, d] fp32. score_type 'none' returns mui only. ``validate`` checks ids / offsets;
-    ``user_out`` is an optional caller-owned fp32 [>= B, K, d] buffer for mui.
+    ``user_out`` is an optional caller-owned fp32 [>= B, K, d] buffer for mui. fp32 tables with
+    pair planes score on the fp16 matrix cores (``x2``, default x2_enabled()), else on the fp32 MFMA.
     """
     st = _lib.SCORE_TYPES.get(score_type)
     if st is None:
@@ -162,11 +208,19 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
             mui = user_out[:B]
         else:
             mui = torch.empty((B, K, d), device=dev, dtype=torch.float32)
+    use_x2 = nt.x2 is not None and dt == _lib.DTYPE_F32 and (x2_enabled() if x2 is None else x2)
     with torch.cuda.device(dev):
-        rc = _lib.lib().miner_score_news(_stream(dev), dt, st, _ptr(nt.table), _ptr(nt.logits), _ptr(nt.proj),
-                                         nt.n_news, _ptr(hid), _ptr(mask), _ptr(his_bias), _ptr(cid), _ptr(offs),
-                                         B, L, C, d, K, _ptr(scores), _ptr(mui))
-    _lib.check(rc, "miner_score_news")
+        if use_x2:
+            px = nt.x2
+            rc = _lib.lib().miner_score_news_x2(_stream(dev), st, _ptr(px.table2), _ptr(px.table_ws), _ptr(nt.logits),
+                                                _ptr(px.proj2), _ptr(px.proj_ws), nt.n_news, _ptr(hid), _ptr(mask),
+                                                _ptr(his_bias), _ptr(cid), _ptr(offs), B, L, C, d, K, _ptr(scores),
+                                                _ptr(mui))
+        else:
+            rc = _lib.lib().miner_score_news(_stream(dev), dt, st, _ptr(nt.table), _ptr(nt.logits), _ptr(nt.proj),
+                                             nt.n_news, _ptr(hid), _ptr(mask), _ptr(his_bias), _ptr(cid), _ptr(offs),
+                                             B, L, C, d, K, _ptr(scores), _ptr(mui))
+    _lib.check(rc, "miner_score_news_x2" if use_x2 else "miner_score_news")
     if st == _lib.SCORE_NONE:
         return mui
     return (scores, mui) if return_user else scores

@@ -23,10 +23,14 @@ def _run(*args):
 
 def test_launcher_two_ranks():
     line = _run("--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1")
-    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["scaling"] == "weak"
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["scaling"] == "strong"
     assert line["value"] > 0 and line["ms_per_step"] > 0
+    # BASELINE config 3: ONE 3M-impression set sharded over the ranks, contiguous and complete
+    assert line["config"]["global_batch"] == 3_000_000
+    assert [tuple(s) for s in line["config"]["shards"]] == [(0, 1_500_000), (1_500_000, 1_500_000)]
 
 
 def test_single_rank_default():
     line = _run("--dry-run", "--steps", "2", "--warmup", "0")
     assert line["n_gpus"] == 1
+    assert line["config"]["global_batch"] == 3_000_000

@@ -80,9 +80,14 @@ def _ok(x, ref, dtype, what):
     return worst
 
 
+FP32_KERNELS = ["x2", "mfma32"]     # fp16-pair operands on the fp16 MFMA (default) / fp32 MFMA (news_score32)
+
+
 # ---- parity against the reference's own outputs (fp32) ------------------------------------------
+@pytest.mark.parametrize("kern", FP32_KERNELS)
 @pytest.mark.parametrize("name", news_golden_names())
-def test_fp32_matches_reference(name):
+def test_fp32_matches_reference(name, kern, monkeypatch):
+    monkeypatch.setenv("MINER_NEWS_FP32", kern)
     g = load_golden(name)
     weighted = g["score_type"] == "weighted"
     W2 = _dev(g["W2"]) if "W2" in g else None
@@ -100,19 +105,10 @@ def test_fp32_bf16x6_matches_reference(name, monkeypatch):
     """The optional bf16x6 form of the fp32 kernel (MINER_NEWS_F32X6=1: every fp32 operand cut exactly
     into three bf16 terms, six bf16 MFMAs per contraction) at the same fp32 bar as the default."""
     monkeypatch.setenv("MINER_NEWS_F32X6", "1")
-    test_fp32_matches_reference(name)
+    test_fp32_matches_reference(name, "mfma32", monkeypatch)
 
 
-@pytest.mark.parametrize("x6", [False, True])
-def test_fp32_config3_vs_f64(x6, monkeypatch):
-    """Config-3 shape (L=50, C=40, K=32, d=768) against a float64 evaluation of the same products:
-    both fp32 forms (fp32 MFMA fma chains, bf16x6) stay well inside the fp32 parity bar."""
-    if x6:
-        monkeypatch.setenv("MINER_NEWS_F32X6", "1")
-    table, hid, mask, cid, offs, W1, Q, W2 = _setup(33, 300, 50, 768, 5000, torch.float32)
-    nt = news.precompute(table, W1, Q, W2)
-    scores = news.score(nt, hid, mask, cid)
-    torch.cuda.synchronize()
+def _f64_scores(table, hid, mask, cid, W1, Q, W2, score_type="weighted"):
     T = table.double().cpu()
     E, Cd = T[hid.cpu().long()], T[cid.cpu().long()]
     w1, q, w2 = (x.double().cpu() for x in (W1, Q, W2))
@@ -122,9 +118,49 @@ def test_fp32_config3_vs_f64(x6, monkeypatch):
     mui = torch.einsum("blk,bld->bkd", a, E)
     x = torch.nn.functional.gelu(mui @ w2.T)
     m = Cd @ mui.transpose(1, 2)
+    if score_type == "max":
+        return m.max(-1).values
     lg = torch.softmax(Cd @ x.transpose(1, 2), dim=-1)
-    ref = (lg * m).sum(-1)
-    _ok(scores, ref, torch.float32, f"config-3 fp32 (x6={x6}) vs float64")
+    return (lg * m).sum(-1)
+
+
+@pytest.mark.parametrize("form", ["x2", "mfma32", "x6"])
+def test_fp32_config3_vs_f64(form, monkeypatch):
+    """Config-3 shape (L=50, C=40, K=32, d=768) against a float64 evaluation of the same products:
+    every fp32 form (fp16 pairs on the fp16 MFMA, fp32 MFMA fma chains, bf16x6) stays well inside
+    the fp32 parity bar."""
+    monkeypatch.setenv("MINER_NEWS_FP32", "x2" if form == "x2" else "mfma32")
+    if form == "x6":
+        monkeypatch.setenv("MINER_NEWS_F32X6", "1")
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(33, 300, 50, 768, 5000, torch.float32)
+    nt = news.precompute(table, W1, Q, W2)
+    scores = news.score(nt, hid, mask, cid)
+    torch.cuda.synchronize()
+    ref = _f64_scores(table, hid, mask, cid, W1, Q, W2)
+    _ok(scores, ref, torch.float32, f"config-3 fp32 ({form}) vs float64")
+
+
+@pytest.mark.parametrize("scale,score_type", [(1.0, "weighted"), (3e3, "max"), (2e-4, "weighted")])
+def test_x2_error_vs_fp32_mfma(scale, score_type, monkeypatch):
+    """The fp16-pair kernel is as accurate as the fp32-MFMA kernel: against float64, its worst and
+    rms score errors stay within 1.5x those of the exact fp32 fma chains (tables scaled by 3e3 and
+    2e-4 exercise the power-of-two pair scale; at 3e3 the 'weighted' softmax over K is one-hot and
+    ill-conditioned in any fp32 form, so that scale is checked on 'max')."""
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(34, 400, 50, 768, 6000, torch.float32)
+    table = table * scale
+    ref = _f64_scores(table, hid, mask, cid, W1, Q, W2, score_type)
+    errs = {}
+    for kern in FP32_KERNELS:
+        monkeypatch.setenv("MINER_NEWS_FP32", kern)
+        nt = news.precompute(table, W1, Q, W2)
+        s = news.score(nt, hid, mask, cid, score_type=score_type)
+        torch.cuda.synchronize()
+        e = (s.double().cpu() - ref).abs()
+        errs[kern] = (float(e.max()), float(e.pow(2).mean().sqrt()))
+        _ok(s, ref, torch.float32, f"{kern} at table scale {scale}")
+    rms = float(ref.pow(2).mean().sqrt())
+    assert errs["x2"][0] <= 1.5 * errs["mfma32"][0] + 1e-7 * rms, errs
+    assert errs["x2"][1] <= 1.5 * errs["mfma32"][1] + 1e-8 * rms, errs
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -148,7 +184,7 @@ def test_precompute_vs_f64(dtype, d, Dc, K):
 
 
 # ---- shapes and layouts against the oracle --------------------------------------------------------
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", ["x2", "mfma32", torch.bfloat16])
 @pytest.mark.parametrize("B,L,d,C,K,Dc", [
     (300, 50, 768, 40, 32, 200),     # config 3 shape
     (700, 50, 256, 40, 32, 200),     # config 2 shape, several impressions per workgroup
@@ -157,7 +193,10 @@ def test_precompute_vs_f64(dtype, d, Dc, K):
     (64, 1, 192, 1, 32, 72),         # L = 1, C = 1
     (40, 37, 320, 150, 12, 64),      # three candidate passes
 ])
-def test_vs_oracle(dtype, B, L, d, C, K, Dc):
+def test_vs_oracle(dtype, B, L, d, C, K, Dc, monkeypatch):
+    if isinstance(dtype, str):
+        monkeypatch.setenv("MINER_NEWS_FP32", dtype)
+        dtype = torch.float32
     table, hid, mask, cid, offs, W1, Q, W2 = _setup(B + d, B, L, d, 2000, dtype, C=C, K=K, Dc=Dc)
     nt = news.precompute(table, W1, Q, W2)
     s, mui = news.score(nt, hid, mask, cid, return_user=True)
@@ -168,8 +207,11 @@ def test_vs_oracle(dtype, B, L, d, C, K, Dc):
 
 
 @pytest.mark.parametrize("score_type", ["weighted", "max", "mean"])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_ragged_bias(score_type, dtype):
+@pytest.mark.parametrize("dtype", ["x2", "mfma32", torch.bfloat16])
+def test_ragged_bias(score_type, dtype, monkeypatch):
+    if isinstance(dtype, str):
+        monkeypatch.setenv("MINER_NEWS_FP32", dtype)
+        dtype = torch.float32
     table, hid, mask, cid, offs, W1, Q, W2 = _setup(7, 211, 50, 768, 3000, dtype, ragged=(0, 150))
     bias = torch.rand(hid.shape, device=DEV) - 0.5
     w2 = W2 if score_type == "weighted" else None
@@ -191,10 +233,11 @@ def test_mui_only_and_all_padded():
     _ok(mui, ref_mui, torch.float32, "mui")
 
 
-def test_launch_invariance_bf16():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_launch_invariance(dtype):
     """A big launch equals the same impressions scored a few at a time (bit-exact: the per-impression
     arithmetic does not depend on the workgroup an impression lands on)."""
-    table, hid, mask, cid, offs, W1, Q, W2 = _setup(9, 3000, 50, 768, 20000, torch.bfloat16)
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(9, 3000, 50, 768, 20000, dtype)
     nt = news.precompute(table, W1, Q, W2)
     big = news.score(nt, hid, mask, cid)
     parts = torch.cat([news.score(nt, hid[i:i + 37], mask[i:i + 37], cid[i:i + 37]) for i in range(0, 3000, 37)])

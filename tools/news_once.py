@@ -1,6 +1,9 @@
 """Run the news-path scoring kernel `reps` times at config-3 shape (for rocprofv3 passes).
 
-    python tools/news_once.py [fp32|bf16] [B] [reps]
+    python tools/news_once.py [fp32|bf16] [B] [reps] [d] [n_news]
+
+fp32 runs the fp16-pair kernel news_score_x2 unless MINER_NEWS_FP32=mfma32 (news_score32). d = 256
+with n_news = 65238 is config 2.
 """
 import os
 import sys
@@ -14,7 +17,9 @@ dev = "cuda:0"
 dt = torch.float32 if (len(sys.argv) < 2 or sys.argv[1] == "fp32") else torch.bfloat16
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 131072
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-n_news, L, C, d, K, Dc = 104000, 50, 40, 768, 32, 200
+d = int(sys.argv[4]) if len(sys.argv) > 4 else 768
+n_news = int(sys.argv[5]) if len(sys.argv) > 5 else 104000
+L, C, K, Dc = 50, 40, 32, 200
 g = torch.Generator(device=dev).manual_seed(36)
 table = (torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5).to(dt)
 lens = torch.randint(0, L + 1, (B,), generator=g, device=dev)

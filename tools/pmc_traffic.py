@@ -56,8 +56,15 @@ def main():
                     help="the news-path scoring kernel news_score<bf16, weighted, dense> (bench.py config3)")
     ap.add_argument("--news32", action="store_true",
                     help="the fp32 news-path scoring kernel news_score32<weighted, dense> (the bench headline)")
+    ap.add_argument("--tag", action="append", default=None,
+                    help="kernel-name substrings to match (mangled and demangled), with --workload / --kernel-name")
+    ap.add_argument("--workload", default=None)
+    ap.add_argument("--kernel-name", default=None)
     args = ap.parse_args()
     workload, kernel = "L50_K32_d768_Dc200_C40_bf16", "miner_fused<bf16,full>"
+    if args.tag:
+        KERNEL_TAGS[:] = args.tag
+        workload, kernel = args.workload, args.kernel_name or args.tag[0]
     if args.news:
         KERNEL_TAGS[:] = ["news_scoreIDF16bLi0ELb0E", "news_score<__bf16, 0, false>"]
         workload, kernel = "news_L50_K32_d768_C40_N104000_bf16", "news_score<bf16,weighted>"
