@@ -86,7 +86,10 @@ int miner_score_news(void* stream, int dtype, int score_type, const void* news_t
  *   Apply it to the news table (the x2 table) and to miner_news_precompute's fp32 news_proj.
  * miner_score_news_x2: miner_score_news (fp32) from the pair tables: table_scale / proj_scale are
  *   the workspaces of the two splits (proj2 / proj_scale NULL unless score_type == WEIGHTED).
- *   Same limits, plus n_news·d·4 < 2^32 (32-bit row offsets).
+ *   Same limits, plus n_news·d·4 < 2^32 (32-bit row offsets). disagree_out [B] fp32 or NULL:
+ *   the eval loss's per-impression disagreement term, mean over k != k' of cos(mui_k, mui_k') with
+ *   the diagonal zeroed (src/loss.py:81, src/utils.py:9-29), formed in the kernel from the Gram
+ *   matrix of mui (no mui is written unless user_out is given).
  */
 size_t miner_news_x2_workspace_floats(void);
 int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* workspace);
@@ -94,7 +97,8 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
                         const float* news_logits, const void* proj2, const float* proj_scale,
                         int n_news, const int32_t* his_ids, const uint8_t* his_mask,
                         const float* his_bias, const int32_t* cand_ids, const int32_t* cand_offsets,
-                        int B, int L, int C, int d, int K, float* scores, float* user_out);
+                        int B, int L, int C, int d, int K, float* scores, float* user_out,
+                        float* disagree_out);
 
 /* 0 if (dtype, L, d, Dc, K) is supported by the news path, else the MINER_E* code. Host-only. */
 int miner_news_supported(int dtype, int L, int d, int Dc, int K);

@@ -50,7 +50,7 @@ SIGNATURES = {
     "miner_news_supported": (_I, [_I, _I, _I, _I, _I]),
     "miner_news_x2_workspace_floats": (ctypes.c_size_t, []),
     "miner_news_split_x2": (_I, [_P, _P, _I, _I, _P, _P]),
-    "miner_score_news_x2": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "miner_score_news_x2": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     # include/miner_wide.h
     "miner_score_wide": (_I, [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P]),
     "miner_wide_proj": (_I, [_P, _I, _P, _P, _I, _I, _P]),

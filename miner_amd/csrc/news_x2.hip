@@ -75,7 +75,9 @@ constexpr int kOffLog = kOffF + kFB;
 constexpr int kOffL1 = kOffLog + 2 * kLogB;
 constexpr int kOffL0 = kOffL1 + 4 * kL1B;
 constexpr int kOffPrep = kOffL0 + 8 * kL0B;
-constexpr int kX2Lds = kOffPrep + 2 * kPrepB;
+constexpr int kOffGram = kOffPrep + 2 * kPrepB;   // eval loss: one wave's Gram partial (3 16x16 tiles) + 32 norms
+constexpr int kGramB = 3 * 256 * 4 + 32 * 4;
+constexpr int kX2Lds = kOffGram + kGramB;
 static_assert(kX2Lds <= 160 * 1024, "news_score_x2 LDS");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -220,6 +222,20 @@ __global__ __launch_bounds__(256) void x2_split(const float* __restrict__ src, i
 // ================================================================================================
 // per-impression scoring
 // ================================================================================================
+// diagnostic build only (-DMINER_STAMPS): per-wave stage cycles (lane 0 of each wave sums s_memtime
+// deltas; read with miner_news_x2_debug_stage_cycles). The stamps wait for outstanding LDS reads.
+#ifdef MINER_STAMPS
+__device__ unsigned long long g_x2_stage[kWaves][8];
+__device__ unsigned long long g_x2_items;
+#define X2_STAMP_DECL unsigned long long st_acc[8] = {0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define X2_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } while (0)
+#define X2_STAMP_FLUSH(n) do { if ((threadIdx.x & 63) == 0) { for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_x2_stage[threadIdx.x >> 6][i_], st_acc[i_]); if (threadIdx.x == 0) atomicAdd(&g_x2_items, (unsigned long long)(n)); } } while (0)
+#else
+#define X2_STAMP_DECL
+#define X2_STAMP(i) do {} while (0)
+#define X2_STAMP_FLUSH(n) do {} while (0)
+#endif
+
 struct X2Params {
   const void* table2;      // [n_news, d] pairs (x2 layout), scale sc_t
   const float* logits;     // [n_news, K]
@@ -233,6 +249,7 @@ struct X2Params {
   const int32_t* cand_off;
   float* scores;
   float* mui_out;
+  float* dis_out;          // [B] per-impression disagreement (the eval loss's Gram term), or null
   int n_news, B, L, C, d, K, score_type;
 };
 
@@ -244,8 +261,13 @@ __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpre
 
 // NCH: 64-column chunks per row (0: d / 64 at run time). SHP 2: the MIND shape (history L = 50,
 // K = 32 interests) compile-time, no category bias and no mui output (plain scoring: the bench, the
-// eval without the eval loss); SHP 0: run-time L, K.
-template <int ST, bool RAGGED, int NCH, int SHP>
+// eval without the eval loss); SHP 0: run-time L, K. LOSS: also the eval loss's per-impression
+// disagreement D = mean_{k != k'} cos(mui_k, mui_k') (loss.py:81, utils.py:9-29) from the Gram matrix
+// mui·muiᵀ, accumulated per chunk by the mui waves of interest tile 0: they run the history product
+// for both interest tiles (the transposed E reads are shared) and add the 3 Gram tiles of their 32
+// columns; at the pass end wave 2 hands its tiles to wave 0 through LDS, which forms D at the next
+// chunk (no mui is written).
+template <int ST, bool RAGGED, int NCH, int SHP, bool LOSS = false>
 __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
@@ -258,10 +280,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   const int nchunk = NCH > 0 ? NCH : d / kCW;
   const float* const bias = SHP == 2 ? nullptr : p.bias;
   float* const mui_out = SHP == 2 ? nullptr : p.mui_out;
+  float* const dis_out = LOSS ? p.dis_out : nullptr;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = wave >> 2, ch = (wave >> 1) & 1, kt = wave & 1;
   const bool k_live = 16 * kt < KK;
   const bool path_live = P == 0 || WEIGHTED;
+  const bool gram_w = LOSS && P == 0 && kt == 0;         // waves 0 and 2: the Gram of their 32 columns
   const char* tabB = static_cast<const char*>(p.table2);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj2) : tabB;
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
@@ -409,13 +433,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   }
 
   // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kt + i][32 kb + 8g + e]
-  u32x4 aH[2], aL[2];
+  // (aH1 / aL1: interest tile 1, the Gram waves only)
+  u32x4 aH[2], aL[2], aH1[2], aL1[2];
   // softmax over the history (model.py:176-181) of this wave's 16 interests, in registers: lane (g, i)
   // takes the 16 history slots 32 kb + 8g + e, the 4 lane rows combined by permlanes
-  auto softmax_inwave = [&](int i) {
+  auto softmax_inwave = [&](int i, int ktile, u32x4* dH, u32x4* dL) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
-    const int k = 16 * kt + j;
+    const int k = 16 * ktile + j;
     const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
     const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
     float v[16];
@@ -438,8 +463,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     if (k >= KK) inv = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) v[s] *= inv;
-    split8h(v, aH[0], aL[0]);
-    split8h(v + 8, aH[1], aL[1]);
+    split8h(v, dH[0], dL[0]);
+    split8h(v + 8, dH[1], dL[1]);
   };
 
   // ring rows no DMA writes read as zeros; the prologue's first barrier orders these stores first
@@ -465,6 +490,46 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   int pend_off = -1, pend_cnt = 0;
   int t = 0;
+  f32x4 gr[3];                                   // Gram tiles (0,0), (0,1), (1,1) of this wave's columns
+#pragma unroll
+  for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int pend_d = -1;                               // impression whose D is formed at the next chunk (wave 0)
+  bool d_pending = false;                        // wave-uniform: a Gram hand-off is waiting
+  X2_STAMP_DECL
+
+  // D of impression b from the Gram tiles (wave 0: its own + wave 2's from LDS): norms n_k = sqrt(G_kk),
+  // S = Σ_{k != k'} G_kk' / (n_k n_k') over k, k' < K, D = S / K² (the diagonal zeroed as in the reference)
+  auto form_d = [&](int b) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const float* pg = reinterpret_cast<const float*>(smem + kOffGram);
+    float* nrm = reinterpret_cast<float*>(smem + kOffGram + 3 * 256 * 4);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gr[q][e] += pg[(q * 4 + e) * 64 + lane];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (4 * g + e == j) {
+        nrm[j] = sqrtf(gr[0][e]);
+        nrm[16 + j] = sqrtf(gr[2][e]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = 4 * g + e;
+      const float nm0 = nrm[m], nm1 = nrm[16 + m], nn0 = nrm[j], nn1 = nrm[16 + j];
+      if (m != j && m < KK && j < KK) sum += gr[0][e] / (nm0 * nn0);
+      if (m < KK && 16 + j < KK) sum += 2.0f * (gr[1][e] / (nm0 * nn1));
+      if (m != j && 16 + m < KK && 16 + j < KK) sum += gr[2][e] / (nm1 * nn1);
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (lane == 0) dis_out[b] = sum / (float)(KK * KK);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
 
   // S7 (model.py:128-136, :213-214) on the X waves 4-7: wave w candidates [16 (w - 4), +16) of the
   // finished pass, lane (kq, c) interests [8 kq, 8 kq + 8); the two column-half partials summed
@@ -526,6 +591,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const char* slot = smem + (t & 1) * kSlot;
     const char* part = slot + P * kPart;
     f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    [[maybe_unused]] f32x4 hy[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       u32x4 eH[2], eL[2];
@@ -538,6 +604,29 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl) hx[ctl] = mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
+      if (LOSS && (mode & 8)) {
+#pragma unroll
+        for (int ctl = 0; ctl < 2; ++ctl) hy[ctl] = mfma_x2(hy[ctl], eH[ctl], eL[ctl], aH1[kb], aL1[kb]);
+      }
+    }
+    X2_STAMP(4);
+    if (LOSS && (mode & 8)) {
+      // Gram tiles over this wave's 32 columns: the operands of the candidate product's B side
+      // (lane (g, i): columns 4g..4g+3 of both column tiles, interest i) serve as A (rows = k) and B
+      float y0[8], y1[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y0[e] = hx[0][e] * op_scale;
+        y0[4 + e] = hx[1][e] * op_scale;
+        y1[e] = hy[0][e] * op_scale;
+        y1[4 + e] = hy[1][e] * op_scale;
+      }
+      u32x4 g0H, g0L, g1H, g1L;
+      split8h(y0, g0H, g0L);
+      split8h(y1, g1H, g1L);
+      gr[0] = mfma_x2(gr[0], g0H, g0L, g0H, g0L);
+      gr[1] = mfma_x2(gr[1], g0H, g0L, g1H, g1L);
+      gr[2] = mfma_x2(gr[2], g1H, g1L, g1H, g1L);
     }
     if ((mode & 4) && 16 * kt + i < KK) {
       float* dst = mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + i) * d + kCW * cc + 32 * ch + 4 * g;
@@ -570,12 +659,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
       u32x4 bH, bL;
       split8h(x, bH, bL);
+      X2_STAMP(5);
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
         const u32x4 ah = u32x4{cH_[q][0].x, cH_[q][0].y, cH_[q][1].x, cH_[q][1].y};
         const u32x4 al = u32x4{cL_[q][0].x, cL_[q][0].y, cL_[q][1].x, cL_[q][1].y};
         acc[q] = mfma_x2(acc[q], ah, al, bH, bL);
       }
+      X2_STAMP(6);
     }
   };
   using I4 = std::integral_constant<int, 4>;
@@ -598,18 +689,27 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       const int ntile = (max(cntp, 1) + 15) >> 4;
       const bool need_mui = P == 0 && mui_out != nullptr && cp == 0;
       const bool need_c = WITH_CAND && path_live;
-      const int mode = (k_live && path_live && (need_c || need_mui)) ? (1 | (need_c ? 2 : 0) | (need_mui ? 4 : 0)) : 0;
+      const bool need_g = gram_w && dis_out != nullptr && cp == 0;
+      const int mode = (k_live && path_live && (need_c || need_mui || need_g))
+                           ? (1 | (need_c ? 2 : 0) | (need_mui ? 4 : 0) | (need_g ? 8 : 0)) : 0;
       const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
       bool did_s7 = false;
       for (int cc = 0; cc < nchunk; ++cc, ++t) {
+        X2_STAMP(7);
         vm_wait_all();                 // this chunk's rows (and every older DMA) landed for this wave,
+        X2_STAMP(0);
         raw_barrier();                 // then for every wave; the other slot is free
+        X2_STAMP(1);
         if (cc == 0) {
-          did_s7 = WITH_CAND && pend_off >= 0;
-          if (did_s7) s7();
+          did_s7 = (WITH_CAND && pend_off >= 0) || d_pending;
+          if (WITH_CAND && pend_off >= 0) s7();
           pend_off = -1;
+          if (LOSS && pend_d >= 0) form_d(pend_d);
+          pend_d = -1;
+          d_pending = false;
           if (cp == 0) {
-            softmax_inwave(ci);
+            softmax_inwave(ci, kt, aH, aL);
+            if (LOSS && gram_w && dis_out) softmax_inwave(ci, 1, aH1, aL1);
             if (nchunk == 1) {
               raw_barrier();           // every wave has read impression ci's logit rows and coefficients
               issue_L2(ci + 2);
@@ -624,19 +724,36 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
           prep_softmax(ci + 2);
         }
+        X2_STAMP(2);
         if (cc + 1 < nchunk) {
           dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
         } else {
           item_offsets(ni, np, nH, nC, nLv);
           dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
         }
+        X2_STAMP(3);
         compute(ci, cc, mode, ntile);
+      }
+      if (nchunk == 1 && did_s7) raw_barrier();
+      if (LOSS && dis_out && cp == 0) {
+        // the Gram hand-off: wave 2 (columns 32..63 of each chunk) -> LDS -> wave 0 at the next chunk
+        if (gram_w && ch == 1) {
+          const int lane = threadIdx.x & 63;
+          float* pg = reinterpret_cast<float*>(smem + kOffGram);
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pg[(q * 4 + e) * 64 + lane] = gr[q][e];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (gram_w && ch == 0) pend_d = imp_b(ci);
+        d_pending = true;
       }
       if constexpr (WITH_CAND) {
         // pass done: every wave publishes its partial M / Lg [c][k ^ swizzle] into its own block
         // F[P][ch] without a barrier; S7, after the next chunk's barrier, reads them. The next
         // publish is at least one barrier after that S7 (one extra barrier when a pass is one chunk).
-        if (nchunk == 1 && did_s7) raw_barrier();
         const int lane = threadIdx.x & 63;
         const int j = lane & 15, g = lane >> 4;
         if (path_live && k_live) {
@@ -658,9 +775,11 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       cH[0] = nH[0]; cH[1] = nH[1]; cC[0] = nC[0]; cC[1] = nC[1]; cLv = nLv;
     }
   }
+  X2_STAMP_FLUSH(n_i);
   vm_wait_all();
   raw_barrier();
   if (WITH_CAND && pend_off >= 0) s7();
+  if (LOSS && pend_d >= 0) form_d(pend_d);
 }
 
 // ================================================================================================
@@ -682,6 +801,16 @@ inline bool al16(const void* q) { return q == nullptr || (reinterpret_cast<uintp
 int x2_launch(void* stream, const X2Params& prm) {
   void (*kern)(X2Params) = nullptr;
   const bool rg = prm.cand_off != nullptr;
+  if (prm.dis_out) {                   // eval with the eval loss (config/eval_miner.txt: metrics + loss)
+#define X2_PICKL(NCHV)                                                                                       \
+    switch (prm.score_type) {                                                                                \
+      case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, NCHV, 0, true> : news_score_x2<MINER_SCORE_WEIGHTED, false, NCHV, 0, true>; break; \
+      case MINER_SCORE_NONE: kern = news_score_x2<MINER_SCORE_NONE, false, NCHV, 0, true>; break;             \
+      default: kern = rg ? news_score_x2<MINER_SCORE_MAX, true, NCHV, 0, true> : news_score_x2<MINER_SCORE_MAX, false, NCHV, 0, true>; break; \
+    }
+    if (prm.d == 768) { X2_PICKL(12) } else { X2_PICKL(0) }
+#undef X2_PICKL
+  } else {
 #define X2_PICK(NCHV)                                                                                        \
   switch (prm.score_type) {                                                                                  \
     case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, NCHV, 0> : news_score_x2<MINER_SCORE_WEIGHTED, false, NCHV, 0>; break; \
@@ -699,6 +828,7 @@ int x2_launch(void* stream, const X2Params& prm) {
   } else {
     X2_PICK(0)
   }
+  }
 #undef X2_PICK
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kX2Lds);
   if (e != hipSuccess) return (int)e;
@@ -712,6 +842,20 @@ int x2_launch(void* stream, const X2Params& prm) {
 }  // namespace
 
 extern "C" {
+
+#ifdef MINER_STAMPS
+// diagnostic build only: read (and reset) the per-wave stage cycles of news_score_x2;
+// out[8 w + i] = cycles of stage i of wave w summed over workgroups, out[64] = impressions
+int miner_news_x2_debug_stage_cycles(unsigned long long* out) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x2_stage), 64 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_x2_items), sizeof(unsigned long long));
+  unsigned long long z[64] = {0};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_x2_stage), z, 64 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_x2_items), z, sizeof(unsigned long long));
+  return (int)e;
+}
+#endif
 
 size_t miner_news_x2_workspace_floats(void) { return (size_t)kAbsBlocks + 8; }
 
@@ -735,7 +879,7 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
                         const float* news_logits, const void* proj2, const float* proj_scale, int n_news,
                         const int32_t* his_ids, const uint8_t* his_mask, const float* his_bias,
                         const int32_t* cand_ids, const int32_t* cand_offsets, int B, int L, int C, int d, int K,
-                        float* scores, float* user_out) {
+                        float* scores, float* user_out, float* disagree_out) {
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
   if (!table2 || !table_scale || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
   if (L <= 0 || d <= 0 || K <= 0) return MINER_EINVAL;
@@ -745,7 +889,7 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
   if (score_type != MINER_SCORE_NONE) {
     if (!scores || !cand_ids) return MINER_EINVAL;
     if (!cand_offsets && (C < 0 || C > kMaxCand)) return MINER_ESHAPE;
-  } else if (!user_out) {
+  } else if (!user_out && !disagree_out) {
     return MINER_EINVAL;
   }
   if (!al16(table2) || !al16(news_logits) || !al16(proj2)) return MINER_EALIGN;
@@ -753,7 +897,7 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
   X2Params prm{table2, news_logits, proj2, table_scale, proj_scale ? proj_scale : table_scale, his_ids, his_mask, his_bias,
                score_type == MINER_SCORE_NONE ? nullptr : cand_ids,
                score_type == MINER_SCORE_NONE ? nullptr : cand_offsets,
-               scores, user_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type};
+               scores, user_out, disagree_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type};
   return x2_launch(stream, prm);
 }
 

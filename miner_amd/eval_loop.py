@@ -115,6 +115,8 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
             raise ValueError(f"scorer='news': an impression has {max_c} candidates (at most {news.MAX_CAND})")
     use_news = scorer == "news" or (scorer == "auto" and news_ok and max_c <= news.MAX_CAND)
     nt = news.precompute(table, packed, with_proj=score_type == "weighted") if use_news else None
+    # fp32 pair-plane tables: the eval loss's disagreement is formed inside the scoring kernel (no mui)
+    fused_loss = want_loss and use_news and nt.x2 is not None and news.x2_enabled()
     # with the per-candidate bias every candidate is one sample: chunk by samples (mui is [N, K, d])
     mc = max(_max_candidates(offs, beh.n), 1)
     step = chunk if category is None else max(1, chunk // mc)
@@ -122,7 +124,7 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
     # with the per-candidate bias a chunk holds up to step x mc one-candidate samples
     rows = min(step, beh.n) if category is None else min(step * mc, int(offs[-1]))
     mui_buf = torch.empty((max(rows, 1), packed.K, d), device=table.device, dtype=torch.float32) \
-        if (want_loss and use_news) else None
+        if (want_loss and use_news and not fused_loss) else None
     for s in range(0, beh.n, step):
         e = min(s + step, beh.n)
         o0, o1 = int(offs[s]), int(offs[e])
@@ -135,13 +137,19 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
             msk = torch.repeat_interleave(msk, sizes, dim=0)
             bias = category.per_sample(his, msk, cid)
             s_off = torch.arange(o1 - o0 + 1, device=table.device, dtype=torch.int32)
-        if use_news:
+        dis = None
+        if use_news and fused_loss:
+            scores, dis = news.score(nt, his, msk, cid, score_type=score_type, cand_offsets=s_off, his_bias=bias,
+                                     validate=False, disagreement=True)
+            mui = None
+        elif use_news:
             out = news.score(nt, his, msk, cid, score_type=score_type, cand_offsets=s_off, his_bias=bias,
                              return_user=want_loss, validate=False, user_out=mui_buf)
+            scores, mui = out if want_loss else (out, None)
         else:
             out = ops.score_gather(table, his, msk, cid, packed, score_type=score_type, cand_offsets=s_off,
                                    his_bias=bias, return_user=want_loss, validate=False)
-        scores, mui = out if want_loss else (out, None)
+            scores, mui = out if want_loss else (out, None)
         lab = beh.labels[o0:o1]
         if "metrics" in evaluation_info:
             ev.add(scores, lab, beh.impression_ids[s:e], c_off)
@@ -150,7 +158,7 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
         if want_loss:
             partial += evaluation.eval_loss_partials(mui, scores, lab, first_sample=first_sample + o0,
                                                      total_samples=total_samples, cand_offsets=s_off,
-                                                     batch_size=eval_batch_size)
+                                                     batch_size=eval_batch_size, dis=dis)
     loss = distributed.reduce_eval_loss(partial) if want_loss else None
     scores = ev.compute_scores(metric_names, save_result, path) if "metrics" in evaluation_info else None
     return loss, scores

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import os
 import pickle
-from typing import Dict, List, Sequence
+from typing import Optional, Dict, List, Sequence
 
 import numpy as np
 import torch
@@ -254,8 +254,9 @@ def disagreement(mui: Tensor) -> Tensor:
     return g.mean(dim=(1, 2))
 
 
-def eval_loss_partials(mui: Tensor, scores: Tensor, labels: Tensor, *, first_sample: int, total_samples: int,
-                       cand_offsets: Tensor = None, batch_size: int = 32) -> Tensor:
+def eval_loss_partials(mui: Optional[Tensor], scores: Tensor, labels: Tensor, *, first_sample: int,
+                       total_samples: int, cand_offsets: Tensor = None, batch_size: int = 32,
+                       dis: Optional[Tensor] = None) -> Tensor:
     """Numerator and positive count of the reference eval loss for a contiguous run of impressions.
 
     The reference evaluates one sample per (impression, candidate), impression-major, in batches
@@ -266,7 +267,8 @@ def eval_loss_partials(mui: Tensor, scores: Tensor, labels: Tensor, *, first_sam
     numerator is Σ_s D(imp(s)) / n_b(s) + Σ_s -logsigmoid(score_s)·label_s. Both sums decompose
     over impression ranges, so ranks add their partials (``first_sample`` = the global index of
     this run's first sample). Returns a float64 tensor [numerator, positives]; the loss is
-    numerator / positives.
+    numerator / positives. ``dis`` [B]: the per-impression disagreement already formed (the news
+    kernel's fused epilogue, news.score(disagreement=True)); else it is computed from ``mui``.
     """
     dev = scores.device
     if cand_offsets is None:
@@ -276,7 +278,7 @@ def eval_loss_partials(mui: Tensor, scores: Tensor, labels: Tensor, *, first_sam
         sizes = torch.diff(cand_offsets.to(dev, torch.int64))
     s = scores.reshape(-1).double()
     lab = labels.reshape(-1).to(dev).double()
-    D = torch.repeat_interleave(disagreement(mui.float()).double(), sizes)
+    D = torch.repeat_interleave((dis if dis is not None else disagreement(mui.float())).double(), sizes)
     idx = first_sample + torch.arange(s.numel(), device=dev, dtype=torch.int64)
     bstart = (idx // batch_size) * batch_size
     nb = torch.clamp(total_samples - bstart, max=batch_size).double()

@@ -143,7 +143,7 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
 def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[Tensor] = None, *,
           score_type: str = "weighted", cand_offsets: Optional[Tensor] = None,
           his_bias: Optional[Tensor] = None, return_user: bool = False, validate: bool = True,
-          user_out: Optional[Tensor] = None, x2: Optional[bool] = None):
+          user_out: Optional[Tensor] = None, x2: Optional[bool] = None, disagreement: bool = False):
     """Miner.forward after the news encoder (model.py:113-138) for impressions given as news ids.
 
     his_ids [B, L] int, his_mask [B, L] bool (True = real click), cand_ids [B, C] (dense) or [N]
@@ -152,6 +152,9 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
     mui [B, K, d] fp32. score_type 'none' returns mui only. ``validate`` checks ids / offsets;
     ``user_out`` is an optional caller-owned fp32 [>= B, K, d] buffer for mui. fp32 tables with
     pair planes score on the fp16 matrix cores (``x2``, default x2_enabled()), else on the fp32 MFMA.
+    ``disagreement`` (fp32 pair-plane tables only) also returns D [B] fp32, the eval loss's
+    per-impression mean pairwise cosine of the K interests with the diagonal zeroed (loss.py:81),
+    formed in the kernel without writing mui; it is appended to the returned tuple.
     """
     st = _lib.SCORE_TYPES.get(score_type)
     if st is None:
@@ -200,7 +203,7 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
             if ids is not None and ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= nt.n_news):
                 raise ValueError(f"{what} must index the news table [0, {nt.n_news})")
     mui = None
-    if return_user or st == _lib.SCORE_NONE:
+    if return_user or (st == _lib.SCORE_NONE and not disagreement):
         if user_out is not None:        # a caller-owned [>= B, K, d] fp32 buffer, reused across calls
             if user_out.dtype != torch.float32 or user_out.dim() != 3 or user_out.shape[0] < B or \
                     tuple(user_out.shape[1:]) != (K, d) or not user_out.is_contiguous():
@@ -209,18 +212,26 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
         else:
             mui = torch.empty((B, K, d), device=dev, dtype=torch.float32)
     use_x2 = nt.x2 is not None and dt == _lib.DTYPE_F32 and (x2_enabled() if x2 is None else x2)
+    dis = None
+    if disagreement:
+        if not use_x2:
+            raise ValueError("disagreement=True needs an fp32 table with pair planes (news.precompute(x2=True))")
+        dis = torch.empty((B,), device=dev, dtype=torch.float32)
     with torch.cuda.device(dev):
         if use_x2:
             px = nt.x2
             rc = _lib.lib().miner_score_news_x2(_stream(dev), st, _ptr(px.table2), _ptr(px.table_ws), _ptr(nt.logits),
                                                 _ptr(px.proj2), _ptr(px.proj_ws), nt.n_news, _ptr(hid), _ptr(mask),
                                                 _ptr(his_bias), _ptr(cid), _ptr(offs), B, L, C, d, K, _ptr(scores),
-                                                _ptr(mui))
+                                                _ptr(mui), _ptr(dis))
         else:
             rc = _lib.lib().miner_score_news(_stream(dev), dt, st, _ptr(nt.table), _ptr(nt.logits), _ptr(nt.proj),
                                              nt.n_news, _ptr(hid), _ptr(mask), _ptr(his_bias), _ptr(cid), _ptr(offs),
                                              B, L, C, d, K, _ptr(scores), _ptr(mui))
     _lib.check(rc, "miner_score_news_x2" if use_x2 else "miner_score_news")
     if st == _lib.SCORE_NONE:
-        return mui
-    return (scores, mui) if return_user else scores
+        return (mui, dis) if disagreement else mui
+    out = (scores, mui) if return_user else (scores,)
+    if disagreement:
+        out = out + (dis,)
+    return out if len(out) > 1 else out[0]

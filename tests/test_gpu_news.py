@@ -271,3 +271,34 @@ def test_bad_inputs_raise():
         news.score(nt, hid, mask, cid, score_type="sum")
     with pytest.raises(ValueError, match="news path"):
         news.precompute(table[:, :96].contiguous(), W1[:, :96].contiguous(), Q, None, with_proj=False)
+
+
+@pytest.mark.parametrize("B,L,d,C,K,ragged", [
+    (300, 50, 768, 40, 32, None),      # config 3 shape
+    (257, 20, 64, 5, 4, None),         # config 1 shape: one chunk per row, K = 4
+    (90, 64, 128, 33, 16, None),       # L = 64, K = 16 (interest tile 1 empty)
+    (40, 37, 320, 150, 12, None),      # three candidate passes
+    (211, 50, 768, None, 32, (0, 150)),  # ragged 0..150 candidates
+])
+def test_fused_disagreement(B, L, d, C, K, ragged, monkeypatch):
+    """The eval loss's disagreement term formed inside the fp32 scoring kernel (the Gram matrix of
+    mui, no mui written) equals the reference formula on the reference's own mui (float64), and the
+    scores of the loss variant equal the plain kernel's (its run-time-shape form) to an ulp."""
+    monkeypatch.setenv("MINER_NEWS_SHP_RT", "1")
+    from miner_amd import evaluation
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(B + d + K, B, L, d, 2000, torch.float32, C=C or 40, K=K,
+                                                    ragged=ragged)
+    nt = news.precompute(table, W1, Q, W2, x2=True)
+    s_plain = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True)
+    s, dis = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True, disagreement=True)
+    torch.cuda.synchronize()
+    # same arithmetic; hipcc may contract a multiply-add differently in the two instantiations (<= 1 ulp)
+    diff = float((s - s_plain).abs().max())
+    assert diff <= 1e-6 * float(s_plain.pow(2).mean().sqrt()), diff
+    ref_mui, _ = _oracle(table, hid, mask, cid, offs, W1, Q, W2)
+    ref = evaluation.disagreement(ref_mui.double()).float()
+    _ok(dis, ref, torch.float32, "disagreement")
+    # mui-only launch with the loss epilogue (score type 'none')
+    m2, d2 = news.score(nt, hid, mask, score_type="none", x2=True, disagreement=True)
+    torch.cuda.synchronize()
+    _ok(d2, ref, torch.float32, "disagreement (none)")

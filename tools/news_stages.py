@@ -17,6 +17,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 STAGES = ["vm_wait (row DMAs)", "barrier", "item start / softmax / aux", "DMA issue",
           "history product", "gelu + split", "candidate product", "pass end + loop"]
+STAGESX2 = ["vm_wait (row DMAs)", "barrier", "item start / S7 / softmax / aux", "DMA issue",
+            "history product", "scale + gelu + split", "candidate product", "pass end + loop"]
 STAGES16 = ["slot wait + barrier", "item start rest / aux", "softmax phases", "DMA issue", "history product",
             "gelu + frag", "cand product + pass end", "S7"]
 
@@ -25,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--batch", type=int, default=32768)
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "x2"])
     args = ap.parse_args()
     import stage_profile
     if args.build:
@@ -34,7 +36,10 @@ def main():
     os.environ["MINER_HIP_LIB"] = stage_profile.STAMP_LIB
     import torch
     from miner_amd import _lib, news, ops, synthetic
-    fn = _lib.lib().miner_news_debug_stage_cycles
+    x2 = args.dtype == "x2"
+    if x2:
+        args.dtype = "fp32"
+    fn = _lib.lib().miner_news_x2_debug_stage_cycles if x2 else _lib.lib().miner_news_debug_stage_cycles
     fn.argtypes = [ctypes.c_void_p]
     fn.restype = ctypes.c_int
     dev = "cuda:0"
@@ -48,27 +53,29 @@ def main():
     hid[~mask] = 0
     cid = torch.randint(1, n_news, (B, C), generator=g, device=dev, dtype=torch.int32)
     W1, Q, W2 = synthetic.init_weights(36, d, Dc, K, device=dev)
-    nt = news.precompute(table, ops.pack_weights(W1, Q, W2, dtype=dt))
-    news.score(nt, hid, mask, cid, validate=False)
+    nt = news.precompute(table, ops.pack_weights(W1, Q, W2, dtype=dt), x2=x2)
+    news.score(nt, hid, mask, cid, validate=False, x2=x2)
     out = (ctypes.c_ulonglong * 65)()
     fn(out)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 3
     a.record()
     for _ in range(reps):
-        news.score(nt, hid, mask, cid, validate=False)
+        news.score(nt, hid, mask, cid, validate=False, x2=x2)
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
     assert fn(out) == 0
     n = out[64]
-    kind = "bf16 news_score" if args.dtype == "bf16" else \
+    kind = "fp32 news_score_x2 (fp16 pairs)" if x2 else "bf16 news_score" if args.dtype == "bf16" else \
         f"fp32 news_score32 ({'bf16x6' if os.environ.get('MINER_NEWS_F32X6') else 'fp32 MFMA'})"
     print(f"{kind} B={B}: "
           f"{ms:.3f} ms/launch ({ms / B * 131072:.2f} ms per 131k), cycles per impression per workgroup:")
     print(f"  {'stage':28s}" + "".join(f"  wave{w}" for w in range(8)))
     names = STAGES16 if args.dtype == "bf16" else STAGES
-    if args.dtype == "fp32" and not os.environ.get("MINER_NEWS_F32X6"):
+    if x2:
+        names = STAGESX2
+    elif args.dtype == "fp32" and not os.environ.get("MINER_NEWS_F32X6"):
         names = STAGES[:4] + ["S7", "in-wave softmax", "products (history + candidate)", STAGES[7]]
     for i, name in enumerate(names):
         print(f"  {name:28s}" + "".join(f" {out[8 * w + i] / n:6.0f}" for w in range(8)))
