@@ -495,6 +495,24 @@ def run_news(args, rank, world, dev):
                                            kernel="news_score32<weighted, dense, fp32 MFMA, 24 chunks>", mode="mfma32"),
                  "max_abs_diff_vs_headline_x_rms": float(d_ex)}
         del ox
+    # the reference's default eval (config/eval_miner.txt: --evaluation_info metrics loss): the same
+    # kernel with the eval loss's disagreement formed in its epilogue (no mui written)
+    loss_line = None
+    if world == 1 and not args.no_exact:
+        from miner_amd import news as _news
+        hid0, mask0, cid0 = pool[0]
+        res = [None]
+
+        def loss_fn():
+            res[0] = _news.score(nt32, hid0, mask0, cid0, validate=False, x2=True, disagreement=True)
+
+        ms_l = _kernel_ms(loss_fn, 3, 1, dev)
+        assert torch.isfinite(res[0][1]).all()
+        loss_line = {"kernel": "news_score_x2<weighted, dense, 12 chunks, LOSS> (scores + per-impression "
+                               "disagreement D, loss.py:81)", "value": round(B * C / (ms_l / 1e3), 1),
+                     "unit": "pairs/s", "ms_per_launch": round(ms_l, 4), "impressions": B,
+                     "vs_plain_kernel": round(kern32 / ms_l, 4)}
+        del res
     # bf16 throughput mode, same batch and protocol
     table16 = table32.to(torch.bfloat16)
     el16, pre16, kern16, o16, nt16 = measure_news(table16, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
@@ -567,7 +585,7 @@ def run_news(args, rank, world, dev):
         "precompute": {"kernels": "news_pre<fp32> + x2_absmax/x2_split of the table and of proj", "ms": round(pre32, 4),
                        "flops": pre_fl, "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
                        "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
-        "fp32_mfma_exact": exact, "weak_scaling": weak,
+        "fp32_mfma_exact": exact, "eval_with_loss": loss_line, "weak_scaling": weak,
         "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "metric_step": metric_step,
         "dense_rows_kernel": dense, "with_host_tolist": with_host,
         "cpu_baseline": cpu, "auc_parity": auc,
@@ -576,27 +594,39 @@ def run_news(args, rank, world, dev):
 
 
 def dense_kernel_line(dev, B=32768, steps=10):
-    """The fused dense-row kernel (weights per impression, miner_score) on the same shape, for
-    comparison: pairs/s and its MFMA fraction."""
+    """The fused dense-row kernel (the drop-in Miner.score module path, model.py:61-138: weights per
+    impression, miner_score) on the config-3 shape, bf16 and fp32 (the reference's precision), each
+    with its roofline (FLOPs 2LdDc + 2LDcK + 2KLd + 2Kd² + 4CdK + 2CK per impression: MFMA-bound)."""
     from miner_amd import ops, synthetic
-    imp = synthetic.impressions(36, 0, B, L=L, d=D, C=C, device=dev, dtype=torch.bfloat16)
     W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
-    pw = ops.pack_weights(W1, Q, W2, dtype=torch.bfloat16)
-    for _ in range(3):
-        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(steps):
-        ops.score(imp.history, imp.his_mask, imp.candidates, pw)
-    b.record()
-    torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / steps
-    tf = flops_per_impression(L, K, D, DC, C) * B / (ms / 1e3) / 1e12
-    del imp
-    return {"kernel": "miner_fused<bf16,full>", "value": round(B * C / (ms / 1e3), 1), "unit": "pairs/s",
-            "ms_per_launch": round(ms, 4), "impressions": B, "tflops": round(tf, 2),
-            "frac_bf16_peak": round(tf / PEAK_BF16_TFLOPS, 4)}
+    out = {}
+    for name, dt, peak, n in (("bf16", torch.bfloat16, PEAK_BF16_TFLOPS, B), ("fp32", torch.float32, PEAK_F32_TFLOPS,
+                                                                               B // 4)):
+        imp = synthetic.impressions(36, 0, n, L=L, d=D, C=C, device=dev, dtype=dt)
+        pw = ops.pack_weights(W1, Q, W2, dtype=dt)
+        for _ in range(3):
+            ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(steps):
+            ops.score(imp.history, imp.his_mask, imp.candidates, pw)
+        b.record(st)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / steps
+        fl = flops_per_impression(L, K, D, DC, C) * n
+        tf = fl / (ms / 1e3) / 1e12
+        by = bytes_per_impression(L, D, C, 2 if name == "bf16" else 4) * n
+        del imp
+        out[name] = {"kernel": f"miner_fused<{name},full>", "value": round(n * C / (ms / 1e3), 1), "unit": "pairs/s",
+                     "ms_per_launch": round(ms, 4), "impressions": n,
+                     "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
+                                  "frac": round(tf / peak, 4), "flops_per_launch": fl,
+                                  "hbm_frac": round(by / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}}
+    out["note"] = ("Miner.score / Miner.forward's drop-in module path on dense [B, L, d] / [B, C, d] rows: every "
+                   "impression re-reads W1 and W2 (the news-id path precomputes them per news row instead)")
+    return out
 
 
 # ---------------------------------------------------------------------------------------------

@@ -34,8 +34,25 @@ def hipcc() -> str:
 DEBUG_LIB = os.path.join(HERE, "libminer_hip_dbg.so")
 
 
+def _flags(debug: bool) -> list:
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed",
+            *(["-DMINER_NEWS_DEBUG"] if debug else []), "-I", os.path.join(ROOT, "include")]
+
+
+def _stamp(debug: bool) -> str:
+    """Build configuration an object / the library was made with: the target, the flags and the
+    hipcc version. Objects and the library are reused only when it matches."""
+    try:
+        ver = subprocess.run([hipcc(), "--version"], capture_output=True, text=True, timeout=60).stdout.strip()
+    except (OSError, subprocess.SubprocessError, RuntimeError):
+        ver = "unknown"
+    return "\n".join([" ".join(_flags(debug)), ver])
+
+
 def _objdir(debug: bool) -> str:
-    return os.path.join(ROOT, "build", "obj_dbg" if debug else "obj")
+    import hashlib
+    tag = hashlib.sha1(_stamp(debug).encode()).hexdigest()[:12]
+    return os.path.join(ROOT, "build", ("obj_dbg_" if debug else "obj_") + ARCH + "_" + tag)
 
 
 def build_library(force: bool = False, verbose: bool = False, debug: bool = False, jobs: int = None) -> str:
@@ -51,13 +68,15 @@ def build_library(force: bool = False, verbose: bool = False, debug: bool = Fals
     from concurrent.futures import ThreadPoolExecutor
     lib = DEBUG_LIB if debug else LIB
     deps = SOURCES + HEADERS
-    if not force and os.path.exists(lib) and all(os.path.getmtime(lib) >= os.path.getmtime(p) for p in deps):
-        return lib
     od = _objdir(debug)
+    stamp_file = lib + ".buildcfg"
+    stamp_ok = os.path.exists(stamp_file) and open(stamp_file).read() == os.path.basename(od)
+    if not force and stamp_ok and os.path.exists(lib) and \
+            all(os.path.getmtime(lib) >= os.path.getmtime(p) for p in deps):
+        return lib
     os.makedirs(od, exist_ok=True)
     hdr_t = max(os.path.getmtime(h) for h in HEADERS)
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed",
-             *(["-DMINER_NEWS_DEBUG"] if debug else []), "-I", os.path.join(ROOT, "include")]
+    flags = _flags(debug)
 
     def compile_one(src):
         obj = os.path.join(od, os.path.basename(src)[:-4] + ".o")
@@ -84,6 +103,8 @@ def build_library(force: bool = False, verbose: bool = False, debug: bool = Fals
     if res.returncode != 0:
         raise RuntimeError(f"link failed ({res.returncode}):\n{res.stderr[-4000:]}")
     os.replace(tmp, lib)
+    with open(stamp_file, "w") as f:
+        f.write(os.path.basename(od))
     return lib
 
 

@@ -5,7 +5,7 @@
 // is 120M pairs.  Here it is a rank sum with ties counted one half, in exact integer arithmetic:
 //
 //   keys   = the fp32 scores mapped to order-preserving uint32 (+0 and -0 one key)
-//   sort   (key, label) pairs by key (hipCUB radix sort, 4 passes of 8 bits)
+//   sort   (key, label) pairs by key (rocPRIM radix sort, AMD's native device primitives)
 //   groups = runs of equal keys: (pos_g, neg_g) by a reduce-by-key over (label ? 2^32 : 1)
 //   N2     = Σ_g pos_g · (2·negbelow_g + neg_g)      (negbelow = exclusive scan of neg_g)
 //   AUC    = N2 / (2·npos·nneg)                        (NaN when one class is absent)
@@ -14,7 +14,10 @@
 // division; sklearn's trapezoid over the ROC curve is the same quantity.  The workspace is
 // caller-owned device memory (miner_auc_workspace_bytes); nothing synchronises.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/device/device_reduce_by_key.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 #include <math.h>
 
@@ -23,8 +26,11 @@
 
 namespace {
 
+// grid-stride loops in size_t: n is up to 2^31 - 1, so a 32-bit index + stride could wrap
+#define AUC_FOR(i, n) for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)(n); i += (size_t)gridDim.x * blockDim.x)
+
 __global__ void auc_keys(const float* __restrict__ s, uint32_t* __restrict__ key, int n) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  AUC_FOR(i, n) {
     uint32_t b = __float_as_uint(s[i]);
     if (b == 0x80000000u) b = 0u;                       // -0 == +0
     key[i] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
@@ -32,21 +38,21 @@ __global__ void auc_keys(const float* __restrict__ s, uint32_t* __restrict__ key
 }
 
 __global__ void auc_vals(const uint8_t* __restrict__ lab, unsigned long long* __restrict__ v, int n) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+  AUC_FOR(i, n)
     v[i] = lab[i] ? (1ull << 32) : 1ull;
 }
 
 __global__ void auc_negs(const unsigned long long* __restrict__ agg, unsigned long long* __restrict__ neg,
                          const int* __restrict__ nruns, int n) {
-  const int G = *nruns;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+  const size_t G = (size_t)*nruns;
+  AUC_FOR(i, n)
     neg[i] = i < G ? (agg[i] & 0xffffffffull) : 0ull;
 }
 
 __global__ void auc_terms(const unsigned long long* __restrict__ agg, const unsigned long long* __restrict__ below,
                           unsigned long long* __restrict__ term, const int* __restrict__ nruns, int n) {
-  const int G = *nruns;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const size_t G = (size_t)*nruns;
+  AUC_FOR(i, n) {
     unsigned long long t = 0ull;
     if (i < G) {
       const unsigned long long a = agg[i];
@@ -70,25 +76,27 @@ struct AucWs {
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+typedef unsigned long long u64;
+
 hipError_t temp_bytes(int n, size_t& bytes) {
+  const size_t N = (size_t)n;
   bytes = 0;
   size_t b = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                    (const uint8_t*)nullptr, (uint8_t*)nullptr, n);
+  hipError_t e = rocprim::radix_sort_pairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint8_t*)nullptr, (uint8_t*)nullptr, N, 0, 32);
   if (e != hipSuccess) return e;
   bytes = b > bytes ? b : bytes;
   b = 0;
-  e = hipcub::DeviceReduce::ReduceByKey(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                        (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                        (int*)nullptr, hipcub::Sum(), n);
+  e = rocprim::reduce_by_key(nullptr, b, (const uint32_t*)nullptr, (const u64*)nullptr, N, (uint32_t*)nullptr,
+                             (u64*)nullptr, (int*)nullptr, rocprim::plus<u64>(), rocprim::equal_to<uint32_t>());
   if (e != hipSuccess) return e;
   bytes = b > bytes ? b : bytes;
   b = 0;
-  e = hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const unsigned long long*)nullptr, (unsigned long long*)nullptr, n);
+  e = rocprim::exclusive_scan(nullptr, b, (const u64*)nullptr, (u64*)nullptr, (u64)0, N, rocprim::plus<u64>());
   if (e != hipSuccess) return e;
   bytes = b > bytes ? b : bytes;
   b = 0;
-  e = hipcub::DeviceReduce::Sum(nullptr, b, (const unsigned long long*)nullptr, (unsigned long long*)nullptr, n);
+  e = rocprim::reduce(nullptr, b, (const u64*)nullptr, (u64*)nullptr, (u64)0, N, rocprim::plus<u64>());
   if (e != hipSuccess) return e;
   bytes = b > bytes ? b : bytes;
   return hipSuccess;
@@ -144,30 +152,33 @@ int miner_global_auc(void* stream, const float* scores, const uint8_t* labels, i
   unsigned long long* n2 = reinterpret_cast<unsigned long long*>(ws + w.n2);
   unsigned long long* tot = reinterpret_cast<unsigned long long*>(ws + w.tot);
   void* temp = ws + w.temp;
-  const int grid = (int)((N + 255) / 256 < 8192 ? (N + 255) / 256 : 8192);
+  const int grid = (int)(((size_t)N + 255) / 256 < 8192 ? ((size_t)N + 255) / 256 : 8192);
   size_t tb = w.temp_bytes;
   hipError_t e;
 
+  const size_t NN = (size_t)N;
   hipLaunchKernelGGL(auc_keys, dim3(grid), dim3(256), 0, st, scores, keys_in, N);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   tb = w.temp_bytes;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(temp, tb, keys_in, keys_out, labels, lab_out, N, 0, 32, st)) != hipSuccess)
+  if ((e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, labels, lab_out, NN, 0, 32, st)) != hipSuccess)
     return (int)e;
   hipLaunchKernelGGL(auc_vals, dim3(grid), dim3(256), 0, st, lab_out, v, N);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   tb = w.temp_bytes;
-  if ((e = hipcub::DeviceReduce::Sum(temp, tb, v, tot, N, st)) != hipSuccess) return (int)e;
+  if ((e = rocprim::reduce(temp, tb, v, tot, (u64)0, NN, rocprim::plus<u64>(), st)) != hipSuccess) return (int)e;
   tb = w.temp_bytes;
-  if ((e = hipcub::DeviceReduce::ReduceByKey(temp, tb, keys_out, keys_in, v, agg, nruns, hipcub::Sum(), N, st)) != hipSuccess)
+  if ((e = rocprim::reduce_by_key(temp, tb, keys_out, v, NN, keys_in, agg, nruns, rocprim::plus<u64>(),
+                                  rocprim::equal_to<uint32_t>(), st)) != hipSuccess)
     return (int)e;
   hipLaunchKernelGGL(auc_negs, dim3(grid), dim3(256), 0, st, agg, v, nruns, N);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   tb = w.temp_bytes;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(temp, tb, v, below, N, st)) != hipSuccess) return (int)e;
+  if ((e = rocprim::exclusive_scan(temp, tb, v, below, (u64)0, NN, rocprim::plus<u64>(), st)) != hipSuccess)
+    return (int)e;
   hipLaunchKernelGGL(auc_terms, dim3(grid), dim3(256), 0, st, agg, below, v, nruns, N);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   tb = w.temp_bytes;
-  if ((e = hipcub::DeviceReduce::Sum(temp, tb, v, n2, N, st)) != hipSuccess) return (int)e;
+  if ((e = rocprim::reduce(temp, tb, v, n2, (u64)0, NN, rocprim::plus<u64>(), st)) != hipSuccess) return (int)e;
   hipLaunchKernelGGL(auc_final, dim3(1), dim3(64), 0, st, n2, tot, auc_out);
   e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;

@@ -153,7 +153,9 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
         lab = beh.labels[o0:o1]
         if "metrics" in evaluation_info:
             ev.add(scores, lab, beh.impression_ids[s:e], c_off)
-        if predictions is not None:
+        if predictions is not None and "metrics" in evaluation_info:
+            # SlowEvaluator.eval_batch runs only with 'metrics' (trainer.py:286-289): a loss-only eval
+            # writes an empty preds.pkl, as the reference's
             predictions.append((torch.sigmoid(scores.float()), beh.impression_ids[s:e], c_off))
         if want_loss:
             partial += evaluation.eval_loss_partials(mui, scores, lab, first_sample=first_sample + o0,
@@ -195,7 +197,7 @@ def evaluate_fastformer(packed, table: torch.Tensor, beh: "synthetic.Behaviors",
         lab = beh.labels[o0:o1]
         if "metrics" in evaluation_info:
             ev.add(scores, lab, beh.impression_ids[s:e], c_off)
-        if predictions is not None:
+        if predictions is not None and "metrics" in evaluation_info:     # trainer_fastformer.py:325-337
             predictions.append((torch.sigmoid(scores.float()), beh.impression_ids[s:e], c_off))
         if want_loss:
             partial += vanilla_eval_loss_partials(scores, lab)

@@ -51,6 +51,12 @@ def _worker(rank, ws, port, name, outdir):
     part = ev.eval_loss_partials(torch.from_numpy(g["mui"][sl]), torch.from_numpy(g["scores_per_candidate"][sl]),
                                  torch.from_numpy(g["labels"][sl]), first_sample=start * C, total_samples=B * C)
     loss = mdist.reduce_eval_loss(part)
+    # preds.pkl through the multi-rank gather of the eval driver (rank 0 writes it)
+    from miner_amd import eval_loop
+    chunks = [(torch.from_numpy(g["probs_grouped"][sl]).float(), torch.arange(start, start + cnt),
+               torch.from_numpy(offs.astype(np.int32)))]
+    os.makedirs(os.path.join(outdir, "ranks"), exist_ok=True)
+    eval_loop._write_predictions(os.path.join(outdir, "ranks"), chunks, rank)
     res = dict(got, eval_loss=loss)
     torch.save({k: float(v) for k, v in res.items()}, os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
@@ -66,6 +72,15 @@ def test_reduce_metrics_over_ranks_equals_single_process(name, ws):
         for m, key in PER_IMP.items():
             np.testing.assert_allclose(np.loadtxt(os.path.join(td, ev.metric_file(m)), ndmin=1), g[key],
                                        atol=1e-12, equal_nan=True)
+        # preds.pkl from the ranks is byte-identical to the one-process file
+        from miner_amd import eval_loop
+        B, C = g["B"], g["C"]
+        one = [(torch.from_numpy(g["probs_grouped"]).float(), torch.arange(B),
+                torch.from_numpy((np.arange(B + 1) * C).astype(np.int32)))]
+        os.makedirs(os.path.join(td, "one"))
+        eval_loop._write_predictions(os.path.join(td, "one"), one, 0)
+        with open(os.path.join(td, "ranks", "preds.pkl"), "rb") as a, open(os.path.join(td, "one", "preds.pkl"), "rb") as b:
+            assert a.read() == b.read()
     for res in per_rank:
         assert res == per_rank[0]           # every rank holds the same answer
         for k, v in g["metrics"].items():

@@ -283,7 +283,7 @@ def test_bad_inputs_raise():
 def test_fused_disagreement(B, L, d, C, K, ragged, monkeypatch):
     """The eval loss's disagreement term formed inside the fp32 scoring kernel (the Gram matrix of
     mui, no mui written) equals the reference formula on the reference's own mui (float64), and the
-    scores of the loss variant equal the plain kernel's (its run-time-shape form) to an ulp."""
+    scores of the loss variant match the plain kernel's (its run-time-shape form) at the fp32 bar."""
     monkeypatch.setenv("MINER_NEWS_SHP_RT", "1")
     from miner_amd import evaluation
     table, hid, mask, cid, offs, W1, Q, W2 = _setup(B + d + K, B, L, d, 2000, torch.float32, C=C or 40, K=K,
@@ -292,9 +292,8 @@ def test_fused_disagreement(B, L, d, C, K, ragged, monkeypatch):
     s_plain = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True)
     s, dis = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True, disagreement=True)
     torch.cuda.synchronize()
-    # same arithmetic; hipcc may contract a multiply-add differently in the two instantiations (<= 1 ulp)
-    diff = float((s - s_plain).abs().max())
-    assert diff <= 1e-6 * float(s_plain.pow(2).mean().sqrt()), diff
+    # same arithmetic; hipcc may contract a multiply-add differently in the two instantiations
+    _ok(s, s_plain, torch.float32, "loss-variant scores vs the plain kernel")
     ref_mui, _ = _oracle(table, hid, mask, cid, offs, W1, Q, W2)
     ref = evaluation.disagreement(ref_mui.double()).float()
     _ok(dis, ref, torch.float32, "disagreement")
