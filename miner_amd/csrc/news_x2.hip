@@ -77,7 +77,9 @@ constexpr int kOffL0 = kOffL1 + 4 * kL1B;
 constexpr int kOffPrep = kOffL0 + 8 * kL0B;
 constexpr int kOffGram = kOffPrep + 2 * kPrepB;   // eval loss: one wave's Gram partial (3 16x16 tiles) + 32 norms
 constexpr int kGramB = 3 * 256 * 4 + 32 * 4;
-constexpr int kX2Lds = kOffGram + kGramB;
+constexpr int kOffDup = kOffGram + kGramB;     // per L1 slot: slot -> unique-row index (64 B) | U
+constexpr int kDupB = 80;
+constexpr int kX2Lds = kOffDup + 4 * kDupB;
 static_assert(kX2Lds <= 160 * 1024, "news_score_x2 LDS");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -117,11 +119,11 @@ __device__ __forceinline__ void x2_dma_b128(const void* g, unsigned lds) {
 }
 
 // 16-byte chunk swizzle of a staged 256-byte row (16 chunks: hi plane 0..7, lo plane 8..15):
-// chunk slot = chunk ^ x2swz(row). Bits (row bit 2, row bit 0, row bit 1, row bit 3): a bijection
-// on rows 0..15, so the ds_read_b64 candidate operand (16 rows, one chunk, per 32-lane half) is
-// conflict-free; the transposed history reads (rows 8g'..8g'+3 and 8g'+8..8g'+11 of a half, two
-// adjacent chunks) see 8 distinct values of bits 1-3, so their 16 pieces land in 16 chunk slots.
-__host__ __device__ inline int x2swz(int row) { return ((row >> 2) & 1) | ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
+// chunk slot = chunk ^ x2swz(row) = chunk ^ ((row & 7) << 1 | (row >> 3) & 1): a bijection on rows
+// 0..15, so the ds_read_b64 candidate operand (16 rows, one chunk, per 32-lane half) is
+// conflict-free; the transposed history reads (8 consecutive rows 8n..8n+7 of a half, two adjacent
+// chunks) see 8 distinct values of bits 1-3, so their 16 pieces land in 16 chunk slots.
+__host__ __device__ inline int x2swz(int row) { return ((row & 7) << 1) | ((row >> 3) & 1); }
 
 __device__ __forceinline__ f32x4 mfma_h(const u32x4& a, const u32x4& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
@@ -258,6 +260,8 @@ __device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return rein
 __device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + kOffL1 + slot * kL1B + 512); }
 __device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B + 768); }
 __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL0 + slot * kL0B); }
+__device__ __forceinline__ uint8_t* dup_idx(char* smem, int slot) { return reinterpret_cast<uint8_t*>(smem + kOffDup + slot * kDupB); }
+__device__ __forceinline__ int* dup_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffDup + slot * kDupB + 64); }
 
 // NCH: 64-column chunks per row (0: d / 64 at run time). SHP 2: the MIND shape (history L = 50,
 // K = 32 interests) compile-time, no category bias and no mui output (plain scoring: the bench, the
@@ -336,10 +340,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
     }
   };
+  // logit rows of impression i by UNIQUE history row (after its dedupe, below)
   auto issue_L2 = [&](int i) {
     if (i >= n_i) return;
     const int lane = threadIdx.x & 63;
-    const int row = min(8 * wave + (lane >> 3), L - 1);
+    const int U = __builtin_amdgcn_readfirstlane(dup_u(smem, i & 3)[0]);
+    const int row = min(8 * wave + (lane >> 3), U - 1);
     const int piece = min(lane & 7, (KK >> 2) - 1);
     const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
     x2_dma_b128(p.logits + (size_t)id * KK + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
@@ -361,6 +367,30 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     pr[l] = mul;
     pr[64 + l] = add;
   };
+  // History rows that repeat a news id (the left padding: every pad slot is the pad news, reader.py:
+  // 101-110, :369) are gathered once: wave 1 replaces impression i's history ids in L1 by its U
+  // unique ids (first-occurrence order) and records slot -> unique-row index. The softmax stays per
+  // slot (a masked and an unmasked slot of one id keep their own logits); the attention weights of
+  // the slots of one row are summed before the history product (Ā = A·S, softmax_inwave), which is
+  // Σ_l A_l e_id(l) regrouped: rows are fetched and contracted once.
+  auto dedupe = [&](int i) {
+    if (wave != 1 || i >= n_i) return;
+    const int l = threadIdx.x & 63;
+    int* his = l1_his(smem, i & 3);
+    const int id = his[min(l, L - 1)];
+    int first = l;
+    for (int j = 0; j < L; ++j) {
+      const int idj = __builtin_amdgcn_readlane(id, j);
+      first = (idj == id && j < first) ? j : first;
+    }
+    const bool uniq = l < L && first == l;
+    const unsigned long long bal = __ballot(uniq);
+    const int uidx = __popcll(bal & ((1ull << l) - 1ull));
+    const int myu = __builtin_amdgcn_ds_bpermute(first << 2, uidx);
+    if (uniq) his[uidx] = id;
+    dup_idx(smem, i & 3)[l] = (uint8_t)(l < L ? myu : 0);
+    if (l == 0) dup_u(smem, i & 3)[0] = __popcll(bal);
+  };
   // row DMAs of a chunk: wave w issues the 4-row blocks w and 8 + (w ^ 4) of every part (the rows
   // 32..47, live for L = 50 / C = 40, go to the X waves, the mostly-padding rows 48..63 to the mui
   // waves). Lane l fills row 4b + (l >> 4), chunk slot l & 15 from source chunk slot ^ x2swz(row).
@@ -372,17 +402,18 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     int off = 0, cnt = 1;
     if (live) cands(i, off, cnt);
     const int cntp = max(1, min(64, cnt - 64 * pass));
+    const int U = live ? __builtin_amdgcn_readfirstlane(dup_u(smem, i & 3)[0]) : 1;
     lv = 0;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int row0 = 4 * dma_block(jj);
-      if (live && row0 < L) lv |= 1u << jj;
+      if (live && row0 < U) lv |= 1u << jj;
       if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 4u << jj;
       const int row = row0 + (lane >> 4);
       const uint32_t poff = (uint32_t)(((lane & 15) ^ x2swz(row)) << 4);
       int h = 0, c = 0;
       if (live) {
-        h = l1_his(smem, i & 3)[min(row, L - 1)];
+        h = l1_his(smem, i & 3)[min(row, U - 1)];
         if (WITH_CAND) c = l1_cand(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
       }
       h = min(max(h, 0), p.n_news - 1);
@@ -409,10 +440,11 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   };
 
   // ---- per-lane LDS read offsets (fixed for the launch) ----
-  // transposed history reads: lane 4q + p of group g supplies row 8g + 4r + q (read r = 0, 1; + 32 kb
-  // rows = 8192 B by immediate), columns 4p .. 4p + 3 of column tile 2ch + ctl; lane i of the group
-  // receives column i of the 4 rows. Candidate reads: row i (+ 16 ct rows = 4096 B), columns
-  // 32 ch + 16 ctl + 4g .. + 3 (8 B).
+  // transposed history reads: lane 4q + p of group g supplies (unique) row 16r + 4g + q (read r = 0, 1;
+  // + 32 kb rows = 8192 B by immediate), columns 4p .. 4p + 3 of column tile 2ch + ctl; lane i of the
+  // group receives column i of the 4 rows: contraction index 8g + e <-> row 32 kb + 16 (e >> 2) + 4g +
+  // (e & 3), the order of the Ā tiles (softmax_inwave). Candidate reads: row i (+ 16 ct rows = 4096 B),
+  // columns 32 ch + 16 ctl + 4g .. + 3 (8 B).
   uint32_t trH[2][2], trL[2][2], cfH[2], cfL[2];
   {
     const int lane = threadIdx.x & 63;
@@ -421,7 +453,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     for (int ctl = 0; ctl < 2; ++ctl) {
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
-        const int row = 8 * g + 4 * rr + q;
+        const int row = 16 * rr + 4 * g + q;
         const int chunk = 4 * ch + 2 * ctl + (pp >> 1);
         trH[ctl][rr] = row * kRB + ((chunk ^ x2swz(row)) << 4) + 8 * (pp & 1);
         trL[ctl][rr] = row * kRB + (((chunk + 8) ^ x2swz(row)) << 4) + 8 * (pp & 1);
@@ -432,23 +464,31 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     }
   }
 
-  // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kt + i][32 kb + 8g + e]
-  // (aH1 / aL1: interest tile 1, the Gram waves only)
+  // Āᵀ B operand of the history product, fp16 pairs: lane (g, i) holds Ā[16 kt + i][u] for the unique
+  // rows u = 32 kb + 16 (e >> 2) + 4g + (e & 3) (aH1 / aL1: interest tile 1, the Gram waves only)
   u32x4 aH[2], aL[2], aH1[2], aL1[2];
   // softmax over the history (model.py:176-181) of this wave's 16 interests, in registers: lane (g, i)
-  // takes the 16 history slots 32 kb + 8g + e, the 4 lane rows combined by permlanes
+  // takes the 16 history slots 32 lb + 8g + e, the 4 lane rows combined by permlanes; then
+  // Āᵀ[u][k] = Σ_l S[l][u]·A[k][l] with S[l][u] = (slot l is row u), 4 u-tiles x 2 slot blocks x
+  // (A hi, A lo) fp16 MFMAs (S is exact in fp16, the sums fp32)
   auto softmax_inwave = [&](int i, int ktile, u32x4* dH, u32x4* dL) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const int k = 16 * ktile + j;
     const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
     const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
+    const uint8_t* ix = dup_idx(smem, i & 3);
+    uint2 iw[2];
+#pragma unroll
+    for (int lb = 0; lb < 2; ++lb) iw[lb] = *reinterpret_cast<const uint2*>(ix + 32 * lb + 8 * g);
     float v[16];
     float mx = -INFINITY;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int l = 32 * (s >> 3) + 8 * g + (s & 7);
-      v[s] = __builtin_fmaf(lgb[l * 32 + k], pr[l], pr[64 + l]);
+      const uint32_t w = (s & 4) ? iw[s >> 3].y : iw[s >> 3].x;
+      const int u = (w >> (8 * (s & 3))) & 0xff;
+      v[s] = __builtin_fmaf(lgb[u * 32 + k], pr[l], pr[64 + l]);
       mx = fmaxf(mx, v[s]);
     }
     mx = x_rows4_max(mx);
@@ -463,8 +503,37 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     if (k >= KK) inv = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) v[s] *= inv;
-    split8h(v, dH[0], dL[0]);
-    split8h(v + 8, dH[1], dL[1]);
+    u32x4 vH[2], vL[2];
+    split8h(v, vH[0], vL[0]);
+    split8h(v + 8, vH[1], vL[1]);
+    // S operand (A side, rows u = 16 ut + j, contraction = the lane's slots): 1.0h where slot -> u
+    f32x4 ab[4];
+#pragma unroll
+    for (int ut = 0; ut < 4; ++ut) {
+      ab[ut] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int lb = 0; lb < 2; ++lb) {
+        u32x4 sm;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t w = m < 2 ? iw[lb].x : iw[lb].y;
+          const int u0 = (w >> (16 * (m & 1))) & 0xff, u1 = (w >> (16 * (m & 1) + 8)) & 0xff;
+          sm[m] = (u0 == 16 * ut + j ? 0x3C00u : 0u) | (u1 == 16 * ut + j ? 0x3C000000u : 0u);
+        }
+        ab[ut] = mfma_h(sm, vL[lb], ab[ut]);
+        ab[ut] = mfma_h(sm, vH[lb], ab[ut]);
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float y[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[e] = ab[2 * kb][e];
+        y[4 + e] = ab[2 * kb + 1][e];
+      }
+      split8h(y, dH[kb], dL[kb]);
+    }
   };
 
   // ring rows no DMA writes read as zeros; the prologue's first barrier orders these stores first
@@ -475,6 +544,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   raw_barrier();
   issue_L1(0); issue_L1(1); issue_L1(2);
   vm_wait_all();
+  raw_barrier();
+  dedupe(0); dedupe(1);
   raw_barrier();
   issue_L2(0); issue_L2(1);
   prep_softmax(0); prep_softmax(1);
@@ -494,6 +565,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 #pragma unroll
   for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   int pend_d = -1;                               // impression whose D is formed at the next chunk (wave 0)
+  int nkb = 2;                                   // 32-row blocks of unique history rows of the item
   bool d_pending = false;                        // wave-uniform: a Gram hand-off is waiting
   X2_STAMP_DECL
 
@@ -594,6 +666,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     [[maybe_unused]] f32x4 hy[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      if (kb == 1 && nkb < 2) break;    // <= 32 unique history rows: one 32-row block
       u32x4 eH[2], eL[2];
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl) {
@@ -684,6 +757,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     int c_off, c_cnt;
     cands(ci, c_off, c_cnt);
     const int cn = max(1, (c_cnt + 63) >> 6);
+    nkb = __builtin_amdgcn_readfirstlane(dup_u(smem, ci & 3)[0]) > 32 ? 2 : 1;
     for (int cp = 0; cp < cn; ++cp) {
       const int cntp = min(64, c_cnt - 64 * cp);
       const int ntile = (max(cntp, 1) + 15) >> 4;
@@ -710,6 +784,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           if (cp == 0) {
             softmax_inwave(ci, kt, aH, aL);
             if (LOSS && gram_w && dis_out) softmax_inwave(ci, 1, aH1, aL1);
+            dedupe(ci + 2);            // L1 of ci + 2 landed; its logit rows are DMA'd by unique row next
             if (nchunk == 1) {
               raw_barrier();           // every wave has read impression ci's logit rows and coefficients
               issue_L2(ci + 2);
