@@ -482,7 +482,8 @@ constexpr int kOffL1 = kOffLog + 2 * kLogB;
 constexpr int kOffL0 = kOffL1 + 4 * kL1B;
 constexpr int kOffPrep = kOffL0 + 8 * kL0B;
 constexpr int kOffSoft = kOffPrep + 2 * kPrepB;      // cooperative softmax partials [wave][k][max, sum]
-constexpr int kNewsLds = kOffSoft + kWaves * 32 * 2 * 4;
+constexpr int kOffDup = kOffSoft + kWaves * 32 * 2 * 4;   // news_score: U (history groups) per L1 slot
+constexpr int kNewsLds = kOffDup + 4 * 16;
 static_assert(kNewsLds <= kLdsMax, "news_score LDS");
 static_assert(NCfg<__bf16>::NSLOT * NCfg<__bf16>::SLOT == kRingB && NCfg<float>::NSLOT * NCfg<float>::SLOT == kRingB &&
               NCfg<__bf16, 128>::NSLOT * NCfg<__bf16, 128>::SLOT == kRingB &&
@@ -546,6 +547,7 @@ __device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return rein
 __device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + kOffL1 + slot * kL1B + 512); }
 __device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B + 768); }
 __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL0 + slot * kL0B); }
+__device__ __forceinline__ int* grp_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffDup + slot * 16); }
 
 // row DMAs of one chunk for this wave (saddr form: the chunk's scalar base + a 32-bit per-lane row
 // offset), parts E[his] / proj[his] / Cand at M0 = mE, mE + PART, mE + 2 PART; one statement, M0
@@ -696,32 +698,54 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       }
     }
   };
-  auto issue_L2 = [&](int i) {           // logit rows of impression i's history (needs its L1)
+  auto issue_L2 = [&](int i) {           // logit rows of impression i's history groups (needs its dedupe)
     if (i >= n_i) return;
     const int lane = threadIdx.x & 63;
-    const int row = min(8 * wave + (lane >> 3), L - 1);
+    const int U = __builtin_amdgcn_readfirstlane(grp_u(smem, i & 3)[0]);
+    const int row = min(8 * wave + (lane >> 3), U - 1);
     const int piece = min(lane & 7, (KK >> 2) - 1);
     const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
     NEWS_CHK(4, p.logits + (size_t)id * KK + 4 * piece, 16, p.logits, (size_t)p.n_news * KK * 4, sbase + kOffLog + (i & 1) * kLogB + wave * 1024, 1024)
     dma_b128_c(p.logits + (size_t)id * KK + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
   };
-  // masked-softmax coefficients of impression i (needs its L1): s_l = logit_l * mul_l + add_l with
-  // (mul, add) = (1, bias_l) for a click, (0, 1e-30) for a pad slot (model.py:176-180), (0, -inf)
-  // past L; computed by wave 3, read by every wave after the next barrier
-  auto prep_softmax = [&](int i) {
-    if (wave != 3 || i >= n_i) return;
+  // The masked history slots holding the same news id — the left padding: every pad slot is the pad
+  // news, masked (reader.py:101-110, :369) — form one group, gathered and contracted once; the softmax
+  // over the history (model.py:176-181) runs over the U groups with multiplicities m_u, the slots' sum
+  // regrouped. Wave 7 (after its L1 landed) replaces impression i's history ids in L1 by the groups'
+  // ids and writes each group's coefficients (±m, add): s_u = logit + bias with weight m for a click
+  // (+m), s_u = 1e-30 with weight m for a pad slot (-m; model.py:176-180), (0, -inf) past U — and U
+  auto dedupe_prep = [&](int i) {
+    if (wave != 7 || i >= n_i) return;
     const int l = threadIdx.x & 63;
-    const uint32_t mw = l1_mask(smem, i & 3)[l];
-    const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + l) & 3);
+    int* his = l1_his(smem, i & 3);
+    const int ls = min(l, L - 1);
+    const int id = his[ls];
+    const uint32_t mw = l1_mask(smem, i & 3)[ls];
+    const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + ls) & 3);
     const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
-    float mul = 0.f, add = -INFINITY;
-    if (l < L) {
-      mul = keep ? 1.f : 0.f;
-      add = keep ? (p.bias ? l1_bias(smem, i & 3)[l] : 0.f) : 1e-30f;
-    }
+    const float bv = (keep && p.bias) ? l1_bias(smem, i & 3)[ls] : 0.f;
+    // the group: the masked slots holding the first masked slot's news id (a masked slot's logit and
+    // bias never enter its score, model.py:176-180); every other slot is a group of its own
+    const unsigned long long pads = __ballot(l < L && !keep);
+    const int f = pads ? (int)__builtin_ctzll(pads) : 0;
+    const int idf = __builtin_amdgcn_readlane(id, f);
+    const unsigned long long grp = pads & __ballot(id == idf);
+    const int m = ((grp >> l) & 1ull) ? (int)__popcll(grp) : 1;   // read at the group's first slot only
+    const bool uniq = l < L && (((grp >> l) & 1ull) == 0ull || l == f);
+    const unsigned long long bal = __ballot(uniq);
+    const int U = __popcll(bal);
+    const int uidx = __popcll(bal & ((1ull << l) - 1ull));
     float* pr = reinterpret_cast<float*>(smem + kOffPrep + (i & 1) * kPrepB);
-    pr[l] = mul;
-    pr[64 + l] = add;
+    if (uniq) {                          // (±m, add): the sign says click / pad, |.| the multiplicity
+      his[uidx] = id;
+      pr[uidx] = keep ? (float)m : -(float)m;
+      pr[64 + uidx] = keep ? bv : 1e-30f;
+    }
+    if (l >= U) {
+      pr[l] = 0.f;
+      pr[64 + l] = -INFINITY;
+    }
+    if (l == 0) grp_u(smem, i & 3)[0] = U;
   };
   // cooperative softmax over the history (model.py:176-181), one impression ahead: phase 1 — wave w
   // takes history slots [8w, 8w+8), lane (h, k) four of them: partial (max, Σexp) per interest k;
@@ -740,13 +764,14 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
     float x[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] = __builtin_fmaf(reinterpret_cast<const float*>(lg + (l0 + j) * 128)[k], m4[j], a4[j]);
+    for (int j = 0; j < 4; ++j)
+      x[j] = __builtin_fmaf(reinterpret_cast<const float*>(lg + (l0 + j) * 128)[k], m4[j] > 0.f ? 1.f : 0.f, a4[j]);
     if (phase == 1) {
       float m = fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3]));
       float s = 0.f;
       if (m != -INFINITY) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s += nx_exp<T>(x[j] - m);
+        for (int j = 0; j < 4; ++j) s = __builtin_fmaf(fabsf(m4[j]), nx_exp<T>(x[j] - m), s);
       }
       const float mo = both_max(m);      // combine the two lane halves
       const float so = (m == -INFINITY ? 0.f : s * nx_exp<T>(m - mo));
@@ -770,7 +795,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       if (k >= KK) inv = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float a = nx_exp<T>(x[j] - M) * inv;
+        const float a = fabsf(m4[j]) * nx_exp<T>(x[j] - M) * inv;
         if constexpr (sizeof(T) == 2) reinterpret_cast<T*>(lg + (l0 + j) * 128)[k] = (T)a;
         else reinterpret_cast<float*>(lg + (l0 + j) * 128)[k] = a;
       }
@@ -784,11 +809,12 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     int off = 0, cnt = 1;
     if (live) cands(i, off, cnt);
     const int cntp = max(1, min(64, cnt - 64 * pass));
+    const int U = live ? __builtin_amdgcn_readfirstlane(grp_u(smem, i & 3)[0]) : 1;
     lv = 0;                            // live DMA instructions of this wave (dma_chunk, SKIP)
 #pragma unroll
     for (int jj = 0; jj < NI; ++jj) {
       const int row0 = (jj ? w4 + 8 * jj : wave) * Cf::RPI;   // first row of instruction jj
-      if (live && row0 < L) lv |= 1u << jj;
+      if (live && row0 < U) lv |= 1u << jj;
       if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 1u << (NI + jj);
     }
     lv = __builtin_amdgcn_readfirstlane(lv);
@@ -801,7 +827,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       const uint32_t poff = (uint32_t)(((lane % Cf::PPR) ^ nswz<T, CW>(rowp)) << 4);
       int h = 0, c = 0;
       if (live) {
-        h = hid[min(rowp, L - 1)];
+        h = hid[min(rowp, U - 1)];
         if (WITH_CAND) c = cid[min(64 * pass + min(rowp, cntp - 1), kMaxCand - 1)];
       }
       h = min(max(h, 0), p.n_news - 1);
@@ -879,7 +905,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     const int r = lane & 31, h = lane >> 5;
     const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
     const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
-    float v[32];
+    float v[32], wm[32];
     float mx = -INFINITY;
 #pragma unroll
     for (int ls = 0; ls < 2; ++ls) {
@@ -891,8 +917,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
         const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float s = __builtin_fmaf(lgb[(l0 + u) * 32 + r], m4[u], a4[u]);
+          const float s = __builtin_fmaf(lgb[(l0 + u) * 32 + r], m4[u] > 0.f ? 1.f : 0.f, a4[u]);
           v[16 * ls + 4 * j4 + u] = s;
+          wm[16 * ls + 4 * j4 + u] = fabsf(m4[u]);
           mx = fmaxf(mx, s);
         }
       }
@@ -901,7 +928,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
-      v[j] = nx_exp<T>(v[j] - mx);     // exp(-inf) = 0 past L
+      v[j] = wm[j] * nx_exp<T>(v[j] - mx);     // exp(-inf) = 0 past U (weight 0)
       sum += v[j];
     }
     sum = both_sum(sum);
@@ -933,8 +960,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   issue_L1(0); issue_L1(1); issue_L1(2);
   vm_wait_all();
   raw_barrier();
+  dedupe_prep(0); dedupe_prep(1);
+  raw_barrier();
   issue_L2(0); issue_L2(1);
-  prep_softmax(0); prep_softmax(1);
   vm_wait_all();
   raw_barrier();
   if (coop) {
@@ -1106,12 +1134,13 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
               load_af(ci);
             } else if constexpr (CW == 64) {
               softmax_inwave(ci);
-              raw_barrier();           // every wave has read impression ci's logit rows
+              dedupe_prep(ci + 2);
+              raw_barrier();           // every wave has read impression ci's logit rows; ci + 2 grouped
               issue_L2(ci + 2);
             }
             issue_L0(ci + 4);
             issue_L1(ci + 3);
-            prep_softmax(ci + 2);
+            if (coop) dedupe_prep(ci + 2);   // its logit rows go out at the next chunk
           }
 #pragma unroll
           for (int tl = 0; tl < NT; ++tl) acc[tl] = zero16();

@@ -10,7 +10,7 @@
 // v_mfma_f32_16x16x32_f16 (every fp16 x fp16 product is exact in fp32, the accumulation is fp32;
 // the dropped lo_a·lo_b is below 2⁻²²·|a·b|). The operand error is the fp32 rounding's order, far
 // below the fp32 accumulation error of a 768-long dot product, which both forms share
-// (tests/test_gpu_news_x2.py measures both against float64). Three fp16 MFMAs (48 cycles) replace
+// (tests/test_gpu_news.py measures both against float64). Three fp16 MFMAs (48 cycles) replace
 // the 256 cycles of a 16x16x32 contraction on the fp32 MFMA, and they co-issue with the other
 // wave's VALU. The pair planes of the news table and of its projection take 4 bytes per element,
 // the same as fp32, so the gathered bytes do not grow.
@@ -69,16 +69,16 @@ constexpr int kFB = 4 * 64 * 32 * 4;                   // F[P][ch] [c][k ^ swz] 
 constexpr int kLogB = 64 * 128;                        // 64 history rows x K (<= 32) fp32
 constexpr int kL1B = 4 * 64 * 3 + 4 * kMaxCand;        // his ids | mask words | bias | cand ids
 constexpr int kL0B = 16;
-constexpr int kPrepB = 2 * 64 * 4;                     // softmax (mul | add) per history slot
+constexpr int kPrepB = 2 * 64 * 4;                     // softmax (±multiplicity | add) per history group
 constexpr int kOffF = kRingB;
 constexpr int kOffLog = kOffF + kFB;
 constexpr int kOffL1 = kOffLog + 2 * kLogB;
 constexpr int kOffL0 = kOffL1 + 4 * kL1B;
 constexpr int kOffPrep = kOffL0 + 8 * kL0B;
-constexpr int kOffGram = kOffPrep + 2 * kPrepB;   // eval loss: one wave's Gram partial (3 16x16 tiles) + 32 norms
+constexpr int kOffGram = kOffPrep + 3 * kPrepB;   // eval loss: one wave's Gram partial (3 16x16 tiles) + 32 norms
 constexpr int kGramB = 3 * 256 * 4 + 32 * 4;
-constexpr int kOffDup = kOffGram + kGramB;     // per L1 slot: slot -> unique-row index (64 B) | U
-constexpr int kDupB = 80;
+constexpr int kOffDup = kOffGram + kGramB;     // per L1 slot: U, the unique history rows of the impression
+constexpr int kDupB = 16;
 constexpr int kX2Lds = kOffDup + 4 * kDupB;
 static_assert(kX2Lds <= 160 * 1024, "news_score_x2 LDS");
 
@@ -144,6 +144,22 @@ __device__ __forceinline__ void split2(float x0, float x1, unsigned& hi, unsigne
   asm volatile("" : "+v"(hb));
   const f16x2 hh = __builtin_bit_cast(f16x2, hb);
   const f16x2 l = {(_Float16)(x0 - (float)hh[0]), (_Float16)(x1 - (float)hh[1])};
+  hi = hb;
+  lo = __builtin_bit_cast(unsigned, l);
+}
+// the attention weights w·e·c (w a small integer multiplicity, e = exp, c = kSA / Σ) -> (hi, lo)
+// fp16 pairs with the residual taken from exact products (fma), so a group of m slots carries one
+// rounding of its weight, not the three of w·(e·c) rounded step by step
+__device__ __forceinline__ void split2w(float w0, float e0, float w1, float e1, float c, unsigned& hi,
+                                        unsigned& lo) {
+  const float p0 = e0 * c, p1 = e1 * c;
+  const float q0 = __builtin_fmaf(e0, c, -p0), q1 = __builtin_fmaf(e1, c, -p1);
+  const f16x2 h = {(_Float16)(w0 * p0), (_Float16)(w1 * p1)};
+  unsigned hb = __builtin_bit_cast(unsigned, h);
+  asm volatile("" : "+v"(hb));
+  const f16x2 hh = __builtin_bit_cast(f16x2, hb);
+  const f16x2 l = {(_Float16)__builtin_fmaf(w0, q0, __builtin_fmaf(w0, p0, -(float)hh[0])),
+                   (_Float16)__builtin_fmaf(w1, q1, __builtin_fmaf(w1, p1, -(float)hh[1]))};
   hi = hb;
   lo = __builtin_bit_cast(unsigned, l);
 }
@@ -260,8 +276,8 @@ __device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return rein
 __device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + kOffL1 + slot * kL1B + 512); }
 __device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B + 768); }
 __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL0 + slot * kL0B); }
-__device__ __forceinline__ uint8_t* dup_idx(char* smem, int slot) { return reinterpret_cast<uint8_t*>(smem + kOffDup + slot * kDupB); }
-__device__ __forceinline__ int* dup_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffDup + slot * kDupB + 64); }
+__device__ __forceinline__ int* dup_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffDup + slot * kDupB); }
+__device__ __forceinline__ float* prep_blk(char* smem, int i) { return reinterpret_cast<float*>(smem + kOffPrep + (i % 3) * kPrepB); }
 
 // NCH: 64-column chunks per row (0: d / 64 at run time). SHP 2: the MIND shape (history L = 50,
 // K = 32 interests) compile-time, no category bias and no mui output (plain scoring: the bench, the
@@ -350,46 +366,46 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
     x2_dma_b128(p.logits + (size_t)id * KK + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
   };
-  // masked-softmax coefficients: s_l = logit_l·mul_l + add_l with (1, bias_l) for a click, (0, 1e-30)
-  // for a pad slot (model.py:176-180), (0, -inf) past L
-  auto prep_softmax = [&](int i) {
-    if (wave != 3 || i >= n_i) return;
-    const int l = threadIdx.x & 63;
-    const uint32_t mw = l1_mask(smem, i & 3)[l];
-    const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + l) & 3);
-    const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
-    float mul = 0.f, add = -INFINITY;
-    if (l < L) {
-      mul = keep ? 1.f : 0.f;
-      add = keep ? (bias ? l1_bias(smem, i & 3)[l] : 0.f) : 1e-30f;
-    }
-    float* pr = reinterpret_cast<float*>(smem + kOffPrep + (i & 1) * kPrepB);
-    pr[l] = mul;
-    pr[64 + l] = add;
-  };
-  // History rows that repeat a news id (the left padding: every pad slot is the pad news, reader.py:
-  // 101-110, :369) are gathered once: wave 1 replaces impression i's history ids in L1 by its U
-  // unique ids (first-occurrence order) and records slot -> unique-row index. The softmax stays per
-  // slot (a masked and an unmasked slot of one id keep their own logits); the attention weights of
-  // the slots of one row are summed before the history product (Ā = A·S, softmax_inwave), which is
-  // Σ_l A_l e_id(l) regrouped: rows are fetched and contracted once.
-  auto dedupe = [&](int i) {
-    if (wave != 1 || i >= n_i) return;
+  // The masked history slots holding the same news id — the left padding: every pad slot is the pad
+  // news, masked (reader.py:101-110, :369) — form one group: its row is gathered and contracted once,
+  // and the softmax over the history (model.py:176-181) runs over the U groups with multiplicities,
+  // A_u = m_u·exp(s_u − max) / Σ_v m_v·exp(s_v − max), exactly the slots' sum regrouped. Wave 7 (an
+  // X wave: they wait at the barriers) replaces impression i's history ids in L1 by the groups' ids
+  // (first-occurrence order) and writes each group's coefficients (±m, add): s_u = logit + bias with
+  // weight m for a click (+m), s_u = 1e-30 with weight m for a pad slot (-m; model.py:176-180),
+  // (0, -inf) past U — and U.
+  auto dedupe_prep = [&](int i) {
+    if (wave != 7 || i >= n_i) return;
     const int l = threadIdx.x & 63;
     int* his = l1_his(smem, i & 3);
-    const int id = his[min(l, L - 1)];
-    int first = l;
-    for (int j = 0; j < L; ++j) {
-      const int idj = __builtin_amdgcn_readlane(id, j);
-      first = (idj == id && j < first) ? j : first;
-    }
-    const bool uniq = l < L && first == l;
+    const int ls = min(l, L - 1);
+    const int id = his[ls];
+    const uint32_t mw = l1_mask(smem, i & 3)[ls];
+    const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + ls) & 3);
+    const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
+    const float bv = (keep && bias) ? l1_bias(smem, i & 3)[ls] : 0.f;
+    // the group: the masked slots holding the first masked slot's news id (a masked slot's logit and
+    // bias never enter its score, model.py:176-180); every other slot is a group of its own
+    const unsigned long long pads = __ballot(l < L && !keep);
+    const int f = pads ? (int)__builtin_ctzll(pads) : 0;
+    const int idf = __builtin_amdgcn_readlane(id, f);
+    const unsigned long long grp = pads & __ballot(id == idf);
+    const int m = ((grp >> l) & 1ull) ? (int)__popcll(grp) : 1;   // read at the group's first slot only
+    const bool uniq = l < L && (((grp >> l) & 1ull) == 0ull || l == f);
     const unsigned long long bal = __ballot(uniq);
+    const int U = __popcll(bal);
     const int uidx = __popcll(bal & ((1ull << l) - 1ull));
-    const int myu = __builtin_amdgcn_ds_bpermute(first << 2, uidx);
-    if (uniq) his[uidx] = id;
-    dup_idx(smem, i & 3)[l] = (uint8_t)(l < L ? myu : 0);
-    if (l == 0) dup_u(smem, i & 3)[0] = __popcll(bal);
+    float* pr = prep_blk(smem, i);
+    if (uniq) {                          // (±m, add): the sign says click / pad, |.| the multiplicity
+      his[uidx] = id;
+      pr[uidx] = keep ? (float)m : -(float)m;
+      pr[64 + uidx] = keep ? bv : 1e-30f;
+    }
+    if (l >= U) {                        // every coefficient past the groups (a unique lane may sit there)
+      pr[l] = 0.f;
+      pr[64 + l] = -INFINITY;
+    }
+    if (l == 0) dup_u(smem, i & 3)[0] = U;
   };
   // row DMAs of a chunk: wave w issues the 4-row blocks w and 8 + (w ^ 4) of every part (the rows
   // 32..47, live for L = 50 / C = 40, go to the X waves, the mostly-padding rows 48..63 to the mui
@@ -464,75 +480,43 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     }
   }
 
-  // Āᵀ B operand of the history product, fp16 pairs: lane (g, i) holds Ā[16 kt + i][u] for the unique
-  // rows u = 32 kb + 16 (e >> 2) + 4g + (e & 3) (aH1 / aL1: interest tile 1, the Gram waves only)
+  // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kt + i][u] of the history
+  // groups u = 32 kb + 16 (e >> 2) + 4g + (e & 3) (aH1 / aL1: interest tile 1, the Gram waves only)
   u32x4 aH[2], aL[2], aH1[2], aL1[2];
-  // softmax over the history (model.py:176-181) of this wave's 16 interests, in registers: lane (g, i)
-  // takes the 16 history slots 32 lb + 8g + e, the 4 lane rows combined by permlanes; then
-  // Āᵀ[u][k] = Σ_l S[l][u]·A[k][l] with S[l][u] = (slot l is row u), 4 u-tiles x 2 slot blocks x
-  // (A hi, A lo) fp16 MFMAs (S is exact in fp16, the sums fp32)
+  // softmax over the history groups (model.py:176-181) of this wave's 16 interests, in registers:
+  // lane (g, i) takes 16 groups, the 4 lane rows combined by permlanes
   auto softmax_inwave = [&](int i, int ktile, u32x4* dH, u32x4* dL) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const int k = 16 * ktile + j;
     const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
-    const float* pr = reinterpret_cast<const float*>(smem + kOffPrep + (i & 1) * kPrepB);
-    const uint8_t* ix = dup_idx(smem, i & 3);
-    uint2 iw[2];
-#pragma unroll
-    for (int lb = 0; lb < 2; ++lb) iw[lb] = *reinterpret_cast<const uint2*>(ix + 32 * lb + 8 * g);
-    float v[16];
+    const float* pr = prep_blk(smem, i);
+    float v[16], wm[16];
     float mx = -INFINITY;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int l = 32 * (s >> 3) + 8 * g + (s & 7);
-      const uint32_t w = (s & 4) ? iw[s >> 3].y : iw[s >> 3].x;
-      const int u = (w >> (8 * (s & 3))) & 0xff;
-      v[s] = __builtin_fmaf(lgb[u * 32 + k], pr[l], pr[64 + l]);
+      const int u = 32 * (s >> 3) + 16 * ((s >> 2) & 1) + 4 * g + (s & 3);
+      const float mu = pr[u];
+      wm[s] = fabsf(mu);
+      v[s] = __builtin_fmaf(lgb[u * 32 + k], mu > 0.f ? 1.f : 0.f, pr[64 + u]);
       mx = fmaxf(mx, v[s]);
     }
     mx = x_rows4_max(mx);
     float sum = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      v[s] = expf(v[s] - mx);                // exp(-inf) = 0 past L
-      sum += v[s];
+      v[s] = expf(v[s] - mx);                // exp(-inf) = 0 past U (weight 0)
+      sum = __builtin_fmaf(wm[s], v[s], sum);
     }
     sum = x_rows4_sum(sum);
     float inv = kSA / sum;
     if (k >= KK) inv = 0.f;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) v[s] *= inv;
-    u32x4 vH[2], vL[2];
-    split8h(v, vH[0], vL[0]);
-    split8h(v + 8, vH[1], vL[1]);
-    // S operand (A side, rows u = 16 ut + j, contraction = the lane's slots): 1.0h where slot -> u
-    f32x4 ab[4];
-#pragma unroll
-    for (int ut = 0; ut < 4; ++ut) {
-      ab[ut] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int lb = 0; lb < 2; ++lb) {
-        u32x4 sm;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const uint32_t w = m < 2 ? iw[lb].x : iw[lb].y;
-          const int u0 = (w >> (16 * (m & 1))) & 0xff, u1 = (w >> (16 * (m & 1) + 8)) & 0xff;
-          sm[m] = (u0 == 16 * ut + j ? 0x3C00u : 0u) | (u1 == 16 * ut + j ? 0x3C000000u : 0u);
-        }
-        ab[ut] = mfma_h(sm, vL[lb], ab[ut]);
-        ab[ut] = mfma_h(sm, vH[lb], ab[ut]);
-      }
-    }
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      float y[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        y[e] = ab[2 * kb][e];
-        y[4 + e] = ab[2 * kb + 1][e];
-      }
-      split8h(y, dH[kb], dL[kb]);
+    for (int m = 0; m < 8; ++m) {
+      unsigned h, l;
+      split2w(wm[2 * m], v[2 * m], wm[2 * m + 1], v[2 * m + 1], inv, h, l);
+      dH[m >> 2][m & 3] = h;
+      dL[m >> 2][m & 3] = l;
     }
   };
 
@@ -545,10 +529,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   issue_L1(0); issue_L1(1); issue_L1(2);
   vm_wait_all();
   raw_barrier();
-  dedupe(0); dedupe(1);
+  dedupe_prep(0); dedupe_prep(1);
   raw_barrier();
   issue_L2(0); issue_L2(1);
-  prep_softmax(0); prep_softmax(1);
   vm_wait_all();
   raw_barrier();
   uint32_t cH[2], cC[2], nH[2] = {0u, 0u}, nC[2] = {0u, 0u};
@@ -784,11 +767,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           if (cp == 0) {
             softmax_inwave(ci, kt, aH, aL);
             if (LOSS && gram_w && dis_out) softmax_inwave(ci, 1, aH1, aL1);
-            dedupe(ci + 2);            // L1 of ci + 2 landed; its logit rows are DMA'd by unique row next
+            dedupe_prep(ci + 2);       // L1 of ci + 2 landed; its logit rows are DMA'd by group next
             if (nchunk == 1) {
               raw_barrier();           // every wave has read impression ci's logit rows and coefficients
               issue_L2(ci + 2);
-              prep_softmax(ci + 2);
             }
             issue_L0(ci + 4);
             issue_L1(ci + 3);
@@ -797,7 +779,6 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
         } else if (cc == 1 && cp == 0) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
-          prep_softmax(ci + 2);
         }
         X2_STAMP(2);
         if (cc + 1 < nchunk) {

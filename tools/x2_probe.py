@@ -27,14 +27,17 @@ cid0 = torch.randint(1, 1 << 30, (B, C), generator=g, device=dev, dtype=torch.in
 W1, Q, W2 = synthetic.init_weights(36, d, Dc, K, device=dev)
 pw = ops.pack_weights(W1, Q, W2, dtype=torch.float32)
 st = torch.cuda.current_stream()
-kerns = ["x2"] + (["mfma32"] if os.environ.get("PROBE_MFMA32") else [])
+kerns = ["x2"] + (["mfma32"] if os.environ.get("PROBE_MFMA32") else []) + (["bf16"] if os.environ.get("PROBE_BF16") else [])
 for n in sizes:
     table = torch.randn((n, d), generator=g, device=dev) / d ** 0.5
     hid = torch.where(mask, hid0 % (n - 1) + 1, torch.zeros_like(hid0))
     cid = cid0 % (n - 1) + 1
     for kern in kerns:
         x2 = kern == "x2"
-        nt = news.precompute(table, pw, x2=x2)
+        if kern == "bf16":
+            nt = news.precompute(table.to(torch.bfloat16), ops.pack_weights(W1, Q, W2, dtype=torch.bfloat16))
+        else:
+            nt = news.precompute(table, pw, x2=x2)
         news.score(nt, hid, mask, cid, validate=False, x2=x2)
         ts = []
         for _ in range(reps):
