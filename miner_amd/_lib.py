@@ -44,6 +44,8 @@ SIGNATURES = {
     "miner_encoder_pack": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _P]),
     "miner_encode_users": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "miner_rank_topk": (_I, [_P, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "miner_rank_topk_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
+    "miner_rank_topk_ws": (_I, [_P, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     # include/miner_news.h
     "miner_news_precompute": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _P]),
     "miner_score_news": (_I, [_P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),

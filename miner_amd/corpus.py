@@ -127,8 +127,9 @@ def rank_topk(user_mui: Tensor, user_proj: Optional[Tensor], news: Tensor, topk:
     dev = mui.device
     top_s = torch.empty(U, topk, dtype=torch.float32, device=dev)
     top_i = torch.empty(U, topk, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(_lib.lib().miner_rank_topk_workspace_bytes(U, topk)), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
-        rc = _lib.lib().miner_rank_topk(_stream(dev), dt, st, _ptr(mui), _ptr(proj), _ptr(tab), U, N, d, K, topk,
-                                        _ptr(top_s), _ptr(top_i))
+        rc = _lib.lib().miner_rank_topk_ws(_stream(dev), dt, st, _ptr(mui), _ptr(proj), _ptr(tab), U, N, d, K, topk,
+                                           _ptr(top_s), _ptr(top_i), _ptr(ws))
     _lib.check(rc, "miner_rank_topk")
     return top_s, top_i

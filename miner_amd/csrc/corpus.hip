@@ -445,8 +445,25 @@ struct RkParams {
   const void* news;
   float* top_s;
   int32_t* top_i;
+  float* ws_s;             // S > 1: per (user, news slice) top-k lists [U][S][topk], merged by rk_merge
+  int32_t* ws_i;
   int U, N, d, K, topk, score_type;
 };
+
+// S > 1 (S = 8, grid = 256): the news steps are dealt to S slices (step st of slice s is news step
+// s + S·st) and 8 consecutive user tiles x 8 slices go to the 32 workgroups b that share b % 8 — one
+// XCD under the round-robin placement (speed only, never correctness): workgroup b takes slice
+// (b >> 3) & 7 of the tiles 32 r + 4 (b & 7) + ((b >> 6) & 3), r = 0, 1, ... So an XCD's L2 holds the
+// user rows of 8 users (1.5 MB at K = 64, d = 768, both mui and proj) that its 32 CUs all read,
+// and every news row it fetches serves 8 users; with S = 1 every CU streams its own 2 users' rows
+// (12 MB per XCD, beyond its 4 MB L2) and the table once per 2 users.
+constexpr int kSplit = 8;
+
+// diagnostic builds only (tools/rk_ablate.py): bit 1 no DMAs, 2 no MFMAs, 4 no epilogue, 8 no
+// per-chunk barrier; the results are wrong, only the time is read
+#ifndef MINER_RK_ABL
+#define MINER_RK_ABL 0
+#endif
 
 // image geometry: rows of 128 B, 16-byte chunk c of row `row` at c ^ ((row >> 1) & 7): the 16 rows
 // of a ds_read_b128 lane group (natural or pi order) hit 16 different slots
@@ -472,7 +489,7 @@ struct RkLds {
   static constexpr int kTotal = kOffCnt + 64;
 };
 
-template <class T, int NKT, int SCORE, int NCH = 0>   // NCH: 128-byte d-chunks per row (0: at run time)
+template <class T, int NKT, int SCORE, int NCH = 0, int S = 1>   // NCH: 128-byte d-chunks per row (0: at run time)
 __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kW = SCORE == MINER_SCORE_WEIGHTED;
@@ -481,7 +498,7 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   constexpr int kChunkSlabs = sizeof(T) == 2 ? 2 : 1;
   const int d = NCH > 0 ? NCH * kRowB / (int)sizeof(T) : p.d, K = p.K, N = p.N;
   const int nchunk = NCH > 0 ? NCH : d * (int)sizeof(T) / kRowB;
-  const int nsteps = (N + kNT - 1) / kNT;
+  const int nsteps = ((N + kNT - 1) / kNT + S - 1) / S;            // news steps per slice
   const int ntiles = (p.U + kUT - 1) / kUT;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int uu = wave >> 2, nsub = wave & 3;
@@ -493,15 +510,19 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   const T* __restrict__ mui = static_cast<const T*>(p.mui);
   const T* __restrict__ proj = static_cast<const T*>(p.proj);
   const T* __restrict__ news = static_cast<const T*>(p.news);
-  const int first = blockIdx.x;
+  const int b = blockIdx.x;
+  const int first = S == 1 ? b : 4 * (b & 7) + ((b >> 6) & 3);    // this workgroup's first tile
+  const int tstride = S == 1 ? (int)gridDim.x : 32;
+  const int slice = S == 1 ? 0 : (b >> 3) & 7;
   if (first >= ntiles) return;
-  const int ntile_mine = (ntiles - first + gridDim.x - 1) / gridDim.x;
+  const int ntile_mine = (ntiles - first + tstride - 1) / tstride;
   const int total_chunks = ntile_mine * nsteps * nchunk;
+  auto news_step = [&](int st) { return S == 1 ? st : slice + S * st; };
 
   // chunk sequence: (tile, step, chunk) -> DMA of its A rows (user k-rows) and B rows (news)
   auto issue = [&](int q) {
     const int lane = fresh_lane();
-    const int c = q % nchunk, st = (q / nchunk) % nsteps, ti = first + (q / nchunk / nsteps) * gridDim.x;
+    const int c = q % nchunk, st = news_step((q / nchunk) % nsteps), ti = first + (q / nchunk / nsteps) * tstride;
     char* img = smem + (q & 1) * LD::kStage;
     constexpr int kBlk = (LD::kARows + kNT) * kRowB / 1024;          // 1 KiB DMA blocks per stage
     for (int blk = wave; blk < kBlk; blk += kWaves) {
@@ -526,15 +547,16 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   if (threadIdx.x < 2 * kUT) cnt[threadIdx.x] = 0;
   issue(0);
   int q = 0;
-  for (int ti = first; ti < ntiles; ti += gridDim.x) {
-    for (int st = 0; st < nsteps; ++st) {
+  for (int ti = first; ti < ntiles; ti += tstride) {
+    for (int sl = 0; sl < nsteps; ++sl) {
+      const int st = news_step(sl);
       f32x16 acc[NR][2];
 #pragma unroll
       for (int t = 0; t < NR; ++t) { acc[t][0] = zero16(); acc[t][1] = zero16(); }
       for (int c = 0; c < nchunk; ++c, ++q) {
-        vm_wait_all();
-        __syncthreads();        // chunk q landed; chunk q - 1's stage is free
-        if (q + 1 < total_chunks) issue(q + 1);
+        if (!(MINER_RK_ABL & 1)) vm_wait_all();
+        if (!(MINER_RK_ABL & 8)) __syncthreads();        // chunk q landed; chunk q - 1's stage is free
+        if (!(MINER_RK_ABL & 1) && q + 1 < total_chunks) issue(q + 1);
         const int lane = fresh_lane();
         const int r = lane & 31, h = lane >> 5;
         const char* img = smem + (q & 1) * LD::kStage;
@@ -549,13 +571,20 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
           for (int t = 0; t < NR; ++t) {
             Frag<T> af;
             rk_frag<T>(af, img, (uu * NR + t) * 32 + pi_row(r), c0);
-            mma_slab<T>(acc[t][0], af, bf[0]);
-            mma_slab<T>(acc[t][1], af, bf[1]);
+            if (!(MINER_RK_ABL & 2)) {
+              mma_slab<T>(acc[t][0], af, bf[0]);
+              mma_slab<T>(acc[t][1], af, bf[1]);
+            } else {
+              acc[t][0][0] += __builtin_bit_cast(float, af.q[0][0]);   // keep the reads
+              acc[t][1][0] += __builtin_bit_cast(float, bf[1].q[0][0]);
+            }
           }
         }
       }
       // ---- epilogue: click score of (user uu, news) for this wave's 64 news ----
-      {
+      if (MINER_RK_ABL & 4) {
+        if (acc[0][0][0] == 1234.5f) p.top_s[0] = acc[NR - 1][1][15];
+      } else {
         const int lane = fresh_lane();
         const int r = lane & 31, h = lane >> 5;
         const int user = ti * kUT + uu;
@@ -665,15 +694,74 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
       const int user = ti * kUT + uu;
       if (nsub == 0 && user < p.U) {
         const int lane = fresh_lane();
+        const size_t o = ((size_t)user * S + slice) * p.topk;
+        float* ds = S == 1 ? p.top_s : p.ws_s;
+        int32_t* di = S == 1 ? p.top_i : p.ws_i;
         for (int i = lane; i < p.topk; i += 64) {
           const bool ok = i < cnt[uu];
-          p.top_s[(size_t)user * p.topk + i] = ok ? list_s[uu * kMaxTopk + i] : -INFINITY;
-          p.top_i[(size_t)user * p.topk + i] = ok ? list_i[uu * kMaxTopk + i] : -1;
+          ds[o + i] = ok ? list_s[uu * kMaxTopk + i] : -INFINITY;
+          di[o + i] = ok ? list_i[uu * kMaxTopk + i] : -1;
         }
       }
       __syncthreads();
       if (threadIdx.x < kUT) cnt[threadIdx.x] = 0;
     }
+  }
+}
+
+// the S per-slice lists of a user (each best first, valid entries (id >= 0) first; the slices hold
+// disjoint news, so no two entries tie in the total order) -> its top-k: an entry's rank is its
+// position in its own list plus, per other list, the count of entries better than it (binary
+// search); ranks < topk are written. One wave per user, its lists staged in LDS.
+constexpr int kMergeUsers = 4;
+__global__ __launch_bounds__(256) void rk_merge(const float* __restrict__ ws_s, const int32_t* __restrict__ ws_i, int U,
+                                                int topk, float* __restrict__ top_s, int32_t* __restrict__ top_i) {
+  __shared__ float ms[kMergeUsers][kSplit * kMaxTopk];
+  __shared__ int mi[kMergeUsers][kSplit * kMaxTopk];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int user = blockIdx.x * kMergeUsers + w;
+  if (user >= U) return;                   // wave-uniform; no block barrier below
+  const size_t base = (size_t)user * kSplit * topk;
+  for (int e = lane; e < kSplit * topk; e += 64) {
+    ms[w][e] = ws_s[base + e];
+    mi[w][e] = ws_i[base + e];
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  int cnt[kSplit];
+  int V = 0;
+#pragma unroll
+  for (int a = 0; a < kSplit; ++a) {
+    int c = 0;
+    for (int i0 = 0; i0 < topk; i0 += 64) c += __popcll(__ballot(i0 + lane < topk && mi[w][a * topk + i0 + lane] >= 0));
+    cnt[a] = c;
+    V += c;
+  }
+#pragma unroll
+  for (int a = 0; a < kSplit; ++a) {
+    for (int j = lane; j < cnt[a]; j += 64) {
+      const float s = ms[w][a * topk + j];
+      const int id = mi[w][a * topk + j];
+      int rank = j;
+#pragma unroll
+      for (int o = 0; o < kSplit; ++o) {
+        if (o == a) continue;
+        int lo = 0, hi = cnt[o];
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (better(ms[w][o * topk + mid], mi[w][o * topk + mid], s, id)) lo = mid + 1; else hi = mid;
+        }
+        rank += lo;
+      }
+      if (rank < topk) {
+        top_s[(size_t)user * topk + rank] = s;
+        top_i[(size_t)user * topk + rank] = id;
+      }
+    }
+  }
+  for (int i = min(V, topk) + lane; i < topk; i += 64) {
+    top_s[(size_t)user * topk + i] = -INFINITY;
+    top_i[(size_t)user * topk + i] = -1;
   }
 }
 
@@ -703,13 +791,22 @@ int ue_dispatch(void* stream, const UeParams& prm) {
   return g ? ue_launch<T, 2, true>(stream, prm) : ue_launch<T, 2, false>(stream, prm);
 }
 
+// the split form (S = kSplit news slices, rk_merge) when the caller gave a workspace and the device
+// has the 256 CUs its tile-to-XCD map assumes (MINER_RK_SPLIT=0: the unsplit form for A/B)
+bool rk_split(const RkParams& prm) {
+  const char* ev = getenv("MINER_RK_SPLIT");
+  const bool on = ev && ev[0] == '1';
+  return prm.ws_s != nullptr && prm.ws_i != nullptr && num_cus() == 256 && on;
+}
+
 template <class T, int NKT, int S>
 int rk_launch(void* stream, const RkParams& prm) {
   // d = 768 in 16-bit (config 5): the chunk count compile-time (MINER_RK_NCH_RT: the run-time form)
-  void (*kern)(RkParams) = rk_fused<T, NKT, S>;
+  const bool split = rk_split(prm);
+  void (*kern)(RkParams) = split ? rk_fused<T, NKT, S, 0, kSplit> : rk_fused<T, NKT, S>;
   if constexpr (sizeof(T) == 2) {
     // (a compile-time K = 64 as well measured 3.9 % faster but not bit-identical top-k: not used)
-    if (prm.d == 768 && !getenv("MINER_RK_NCH_RT")) kern = rk_fused<T, NKT, S, 12>;
+    if (prm.d == 768 && !getenv("MINER_RK_NCH_RT")) kern = split ? rk_fused<T, NKT, S, 12, kSplit> : rk_fused<T, NKT, S, 12>;
   }
   constexpr int NR = S == MINER_SCORE_WEIGHTED ? 2 * NKT : NKT;
   const int lds = RkLds<NR>::kTotal;
@@ -717,8 +814,13 @@ int rk_launch(void* stream, const RkParams& prm) {
   if (e != hipSuccess) return (int)e;
   const int ntiles = (prm.U + kUT - 1) / kUT;
   int grid = num_cus();
-  if (grid > ntiles) grid = ntiles;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, static_cast<hipStream_t>(stream), prm);
+  if (!split && grid > ntiles) grid = ntiles;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, prm);
+  e = hipGetLastError();
+  if (e != hipSuccess || !split) return e == hipSuccess ? MINER_OK : (int)e;
+  hipLaunchKernelGGL(rk_merge, dim3((prm.U + kMergeUsers - 1) / kMergeUsers), dim3(64 * kMergeUsers), 0, s, prm.ws_s,
+                     prm.ws_i, prm.U, prm.topk, prm.top_s, prm.top_i);
   e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;
 }
@@ -798,8 +900,20 @@ int miner_encode_users(void* stream, int dtype, const void* history, const int32
   return ue_dispatch<float>(stream, prm);
 }
 
+size_t miner_rank_topk_workspace_bytes(int U, int topk) {
+  if (U <= 0 || topk <= 0 || topk > kMaxTopk) return 0;
+  return (size_t)U * kSplit * topk * 8;
+}
+
 int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
                     const void* news, int U, int N, int d, int K, int topk, float* top_scores, int32_t* top_ids) {
+  return miner_rank_topk_ws(stream, dtype, score_type, user_mui, user_proj, news, U, N, d, K, topk, top_scores, top_ids,
+                            nullptr);
+}
+
+int miner_rank_topk_ws(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
+                       const void* news, int U, int N, int d, int K, int topk, float* top_scores, int32_t* top_ids,
+                       void* workspace) {
   const int ck = check_dims(dtype, d, 1, K);
   if (ck != MINER_OK) return ck;
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_MEAN) return MINER_EINVAL;
@@ -810,7 +924,12 @@ int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mu
   if (!aligned16(user_mui) || !aligned16(user_proj) || !aligned16(news)) return MINER_EALIGN;
   if (U == 0) return MINER_OK;
   RkParams prm{};
+  if (!aligned16(workspace)) return MINER_EALIGN;
   prm.mui = user_mui; prm.proj = user_proj; prm.news = news; prm.top_s = top_scores; prm.top_i = top_ids;
+  if (workspace) {
+    prm.ws_s = static_cast<float*>(workspace);
+    prm.ws_i = reinterpret_cast<int32_t*>(static_cast<char*>(workspace) + (size_t)U * kSplit * topk * 4);
+  }
   prm.U = U; prm.N = N; prm.d = d; prm.K = K; prm.topk = topk; prm.score_type = score_type;
   if (dtype == MINER_DTYPE_BF16) return rk_dispatch<__bf16>(stream, prm);
   if (dtype == MINER_DTYPE_F16) return rk_dispatch<_Float16>(stream, prm);

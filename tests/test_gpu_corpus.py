@@ -126,3 +126,27 @@ def test_argument_errors():
         corpus.rank_topk(z, z, torch.zeros(10, 128, device=DEV), 5, score_type="sum")
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         corpus.rank_topk(z.cpu(), z.cpu(), torch.zeros(10, 128), 5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("U,N,topk", [(2048 // 16, 20000, 100), (3, 200, 256), (37, 5000, 7)])
+def test_split_equals_unsplit(dtype, U, N, topk, monkeypatch):
+    """miner_rank_topk_ws (news slices per XCD-shared user group + rk_merge) returns exactly the
+    unsplit kernel's top-k: the same per-pair arithmetic, a total order (score desc, id asc) and
+    disjoint slices. Duplicated news rows force exact score ties across slices."""
+    gen = torch.Generator().manual_seed(U + N)
+    K, d = 64, 768
+    table = torch.randn(N, d, generator=gen) / d ** 0.5
+    table[N // 2:N // 2 + 50] = table[:50]            # exact ties, ids in different slices
+    mui = (torch.randn(U, K, d, generator=gen) / 4).to(DEV, dtype)
+    proj = (torch.randn(U, K, d, generator=gen) / 4).to(DEV, dtype)
+    tab = table.to(DEV, dtype)
+    for st in ("weighted", "max"):
+        monkeypatch.setenv("MINER_RK_SPLIT", "1")
+        a = corpus.rank_topk(mui, proj, tab, topk, score_type=st)
+        monkeypatch.setenv("MINER_RK_SPLIT", "0")
+        b = corpus.rank_topk(mui, proj, tab, topk, score_type=st)
+        torch.cuda.synchronize()
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), st
+        if N < topk:
+            assert (a[1][:, N:] == -1).all()

@@ -223,6 +223,40 @@ def test_ragged_bias(score_type, dtype, monkeypatch):
     _ok(s, ref, dtype, f"{score_type} scores")
 
 
+@pytest.mark.parametrize("dtype", ["x2", "mfma32", torch.bfloat16])
+def test_masked_slot_groups(dtype, monkeypatch):
+    """The news kernels gather and contract the masked history slots holding one news id (the left
+    padding) once, with a multiplicity (news_x2.hip dedupe_prep). Irregular inputs against the oracle:
+    masks that are not left-aligned, several different ids under the mask, a masked slot sharing a
+    clicked slot's id, repeated clicked ids, all-masked and no-masked histories, with category bias."""
+    if isinstance(dtype, str):
+        monkeypatch.setenv("MINER_NEWS_FP32", dtype)
+        dtype = torch.float32
+    B, L = 240, 50
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(12, B, L, 768, 3000, dtype)
+    g = torch.Generator(device="cpu").manual_seed(12)
+    h = hid.cpu().clone()
+    m = mask.cpu().clone()
+    m[:60] = torch.rand((60, L), generator=g) < 0.5                   # scattered masks
+    h[:60] = torch.randint(0, 6, (60, L), generator=g)                 # few ids: repeats everywhere
+    h[60:120][~m[60:120]] = torch.randint(0, 3, (60, L), generator=g)[~m[60:120]]   # mixed ids under the mask
+    h[120:150, :] = h[120:150, :1]                                     # every slot one id, masked or not
+    m[150:170] = False                                                 # all masked, assorted ids
+    h[150:170] = torch.randint(0, 3000, (20, L), generator=g)
+    m[170:190] = True                                                  # nothing masked
+    bias = torch.rand((B, L), generator=g) - 0.5
+    hid, mask, bias = h.to(DEV), m.to(DEV), bias.to(DEV)
+    nt = news.precompute(table, W1, Q, W2)
+    s, mui = news.score(nt, hid, mask, cid, his_bias=bias, return_user=True)
+    s_plain = news.score(nt, hid, mask, cid)
+    torch.cuda.synchronize()
+    ref_mui, ref = _oracle(table, hid, mask, cid, None, W1, Q, W2, bias=bias)
+    _ok(s, ref, dtype, "scores")
+    _ok(mui, ref_mui, dtype, "mui")
+    _, ref_plain = _oracle(table, hid, mask, cid, None, W1, Q, W2)
+    _ok(s_plain, ref_plain, dtype, "plain scores")
+
+
 def test_mui_only_and_all_padded():
     table, hid, mask, cid, offs, W1, Q, W2 = _setup(8, 50, 30, 256, 500, torch.float32)
     mask[:10] = False                      # all-padded histories: uniform average of pad rows
