@@ -345,6 +345,12 @@ __device__ __forceinline__ void dma_b128(const void* g, unsigned lds) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
                : "=&s"(t) : "v"(g), "s"(lds) : "memory");
 }
+// the same with the default cache policy (lines meant to stay in L2 for other CUs to re-read)
+__device__ __forceinline__ void dma_b128_rt(const void* g, unsigned lds) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(g), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void dma_b32(const void* g, unsigned lds) {
   unsigned t;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"

@@ -460,10 +460,21 @@ struct RkParams {
 constexpr int kSplit = 8;
 
 // diagnostic builds only (tools/rk_ablate.py): bit 1 no DMAs, 2 no MFMAs, 4 no epilogue, 8 no
-// per-chunk barrier; the results are wrong, only the time is read
+// per-chunk barrier (the results are wrong, only the time is read)
 #ifndef MINER_RK_ABL
 #define MINER_RK_ABL 0
 #endif
+#ifndef MINER_RK_DMAW
+#define MINER_RK_DMAW 4   // 91.5 -> 86.9 ms per config-5 step against 8 (tools/rk_ablate.py)
+#endif
+
+// one LDS-DMA (saddr form: scalar base + 32-bit per-lane offset) into M0 = m, M0 saved / restored;
+// default cache policy (nt on the ranker's rows cost 18 %, tools/rk_ablate.py)
+__device__ __forceinline__ void rk_dma(uint32_t off, const char* base, unsigned m) {
+  unsigned t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(t) : "v"(off), "s"(base), "s"(m) : "memory");
+}
 
 // image geometry: rows of 128 B, 16-byte chunk c of row `row` at c ^ ((row >> 1) & 7): the 16 rows
 // of a ds_read_b128 lane group (natural or pi order) hit 16 different slots
@@ -519,33 +530,62 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   const int total_chunks = ntile_mine * nsteps * nchunk;
   auto news_step = [&](int st) { return S == 1 ? st : slice + S * st; };
 
-  // chunk sequence: (tile, step, chunk) -> DMA of its A rows (user k-rows) and B rows (news)
-  auto issue = [&](int q) {
+  // Row DMAs. Wave w issues the 1 KiB blocks w + 8 j of every stage: j < NR are user k-rows (A),
+  // the rest news rows (B). The per-lane byte offsets are fixed for the launch (A: within the user's
+  // [K, d] array; B: from the step's first news row); the user, step and chunk go into the scalar
+  // base of the saddr form. A chunk's blocks are issued spread over the previous chunk's MFMAs.
+  constexpr int kBlk = (LD::kARows + kNT) * kRowB / 1024;          // 1 KiB DMA blocks per stage
+  static_assert(kBlk % kWaves == 0, "whole DMA blocks per wave");
+  constexpr int kJ = kBlk / kWaves;
+  uint32_t voff[kJ];
+#pragma unroll
+  for (int jj = 0; jj < kJ; ++jj) {
     const int lane = fresh_lane();
-    const int c = q % nchunk, st = news_step((q / nchunk) % nsteps), ti = first + (q / nchunk / nsteps) * tstride;
-    char* img = smem + (q & 1) * LD::kStage;
-    constexpr int kBlk = (LD::kARows + kNT) * kRowB / 1024;          // 1 KiB DMA blocks per stage
-    for (int blk = wave; blk < kBlk; blk += kWaves) {
-      const int P = blk * 64 + lane;
-      const int row = P >> 3, pc = P & 7;
-      const int cl = pc ^ rk_swz(row);
-      const T* g;
-      if (row < LD::kARows) {
-        const int ou = row / (NR * 32), t = (row / 32) % NR, rr = row % 32;
-        const int user = min(ti * kUT + ou, p.U - 1);
-        const int k = min(32 * (t % NKT) + rr, K - 1);
-        const T* src = (kW && t >= NKT) ? proj : mui;
-        g = src + ((size_t)user * K + k) * d + c * kEpc<T> + cl * (16 / (int)sizeof(T));
-      } else {
+    const int P = (wave + kWaves * jj) * 64 + lane;
+    const int row = P >> 3, cl = (P & 7) ^ rk_swz(row);
+    if (jj < NR) {
+      const int k = min(32 * (((row >> 5) % NR) % NKT) + (row & 31), K - 1);
+      voff[jj] = (uint32_t)(k * d) * (uint32_t)sizeof(T) + cl * 16;
+    } else {
+      voff[jj] = (uint32_t)((row - LD::kARows) * d) * (uint32_t)sizeof(T) + cl * 16;
+    }
+  }
+  // the next chunk to issue: (tile nti, slice step nsl, chunk nc), advanced after each issue
+  int nti = first, nsl = 0, nc = 0;
+  auto dma_block = [&](int jj, int stage) {
+    const unsigned la = __builtin_amdgcn_readfirstlane(lds_offset(smem + stage * LD::kStage + (wave + kWaves * jj) * 1024));
+    if (jj < NR) {
+      const int row0 = 8 * wave + 64 * jj;
+      const int t = (row0 >> 5) % NR, ou = row0 / (NR * 32);
+      const int user = min(nti * kUT + ou, p.U - 1);
+      const T* src = (kW && t >= NKT) ? proj : mui;
+      rk_dma(voff[jj], reinterpret_cast<const char*>(src + (size_t)user * K * d) + nc * kRowB, la);
+    } else {
+      const int st = news_step(nsl);
+      if (st * kNT + kNT <= N) {
+        rk_dma(voff[jj], reinterpret_cast<const char*>(news + (size_t)st * kNT * d) + nc * kRowB, la);
+      } else {                           // the table's last (partial) step: rows clamped to N - 1
+        const int lane = fresh_lane();
+        const int P = (wave + kWaves * jj) * 64 + lane;
+        const int row = P >> 3, cl = (P & 7) ^ rk_swz(row);
         const int n = min(st * kNT + (row - LD::kARows), N - 1);
-        g = news + (size_t)n * d + c * kEpc<T> + cl * (16 / (int)sizeof(T));
+        dma_b128_rt(news + (size_t)n * d + nc * kEpc<T> + cl * (16 / (int)sizeof(T)), la);
       }
-      dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + blk * 1024)));
+    }
+  };
+  auto advance = [&]() {
+    if (++nc == nchunk) {
+      nc = 0;
+      if (++nsl == nsteps) { nsl = 0; nti += tstride; }
     }
   };
 
   if (threadIdx.x < 2 * kUT) cnt[threadIdx.x] = 0;
-  issue(0);
+  if (!(MINER_RK_ABL & 1)) {
+#pragma unroll
+    for (int jj = 0; jj < kJ; ++jj) dma_block(jj, 0);
+  }
+  advance();
   int q = 0;
   for (int ti = first; ti < ntiles; ti += tstride) {
     for (int sl = 0; sl < nsteps; ++sl) {
@@ -556,11 +596,12 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
       for (int c = 0; c < nchunk; ++c, ++q) {
         if (!(MINER_RK_ABL & 1)) vm_wait_all();
         if (!(MINER_RK_ABL & 8)) __syncthreads();        // chunk q landed; chunk q - 1's stage is free
-        if (!(MINER_RK_ABL & 1) && q + 1 < total_chunks) issue(q + 1);
+        const bool pre = !(MINER_RK_ABL & 1) && q + 1 < total_chunks;
         const int lane = fresh_lane();
         const int r = lane & 31, h = lane >> 5;
         const char* img = smem + (q & 1) * LD::kStage;
         const char* bimg = img + LD::kARows * kRowB;
+        constexpr int kPairs = kChunkSlabs * NR;
 #pragma unroll
         for (int s = 0; s < kChunkSlabs; ++s) {
           const int c0 = sizeof(T) == 2 ? 4 * s + 2 * h : 4 * h;
@@ -578,12 +619,23 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
               acc[t][0][0] += __builtin_bit_cast(float, af.q[0][0]);   // keep the reads
               acc[t][1][0] += __builtin_bit_cast(float, bf[1].q[0][0]);
             }
+            // the next chunk's DMA blocks, spread over this chunk's first kWin MFMA pairs
+            constexpr int kWin = MINER_RK_DMAW < kPairs ? MINER_RK_DMAW : kPairs;
+#pragma unroll
+            for (int jj = 0; jj < kJ; ++jj)
+              if (jj * kWin / kJ == s * NR + t && pre) dma_block(jj, (q + 1) & 1);
           }
         }
+        if (pre) advance();
       }
       // ---- epilogue: click score of (user uu, news) for this wave's 64 news ----
-      if (MINER_RK_ABL & 4) {
-        if (acc[0][0][0] == 1234.5f) p.top_s[0] = acc[NR - 1][1][15];
+      if (MINER_RK_ABL & 4) {            // every accumulator stays live (no MFMA is dead code)
+        float z = 0.f;
+#pragma unroll
+        for (int t = 0; t < NR; ++t)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) z += acc[t][0][e] + acc[t][1][e];
+        if (z == 1234.5f) p.top_s[0] = z;
       } else {
         const int lane = fresh_lane();
         const int r = lane & 31, h = lane >> 5;

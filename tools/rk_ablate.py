@@ -3,7 +3,8 @@
 every build timed interleaved in one process on the same inputs (2048 users x 200k news, K=64, d=768).
 
     python tools/rk_ablate.py --build 0 1 2 4 5 6 7 8     # CPU: tools/bisect/librk_abl<bits>.so
-    python tools/rk_ablate.py 0 1 2 4 5 6 7 8              # GPU
+    python tools/rk_ablate.py 0 1 2 4 5 6 7 8 16s          # GPU; a trailing "s": the split form
+                                                           # (miner_rank_topk_ws, MINER_RK_SPLIT=1)
 """
 import ctypes
 import os
@@ -17,12 +18,16 @@ sys.path.insert(0, ROOT)
 
 
 def build(variants, extra=()):
+    """variant "<bits>" or "<bits>w<W>" (-DMINER_RK_DMAW=W: the next chunk's DMAs within the first W
+    MFMA pairs of a chunk)"""
     from miner_amd.build import hipcc
     os.makedirs(OUT, exist_ok=True)
     for v in variants:
         lib = os.path.join(OUT, f"librk_abl{v}.so")
+        bits, _, w = str(v).partition("w")
+        wdef = [f"-DMINER_RK_DMAW={w}"] if w else []
         subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-pass-failed",
-                        f"-DMINER_RK_ABL={v}", *extra, "-I", os.path.join(ROOT, "include"),
+                        f"-DMINER_RK_ABL={bits}", *wdef, *extra, "-I", os.path.join(ROOT, "include"),
                         os.path.join(ROOT, "miner_amd", "csrc", "corpus.hip"), "-o", lib], check=True)
         print("built", lib, flush=True)
 
@@ -39,15 +44,17 @@ def run(variants, U=2048, N=200000, reps=3):
     ts = torch.empty(U, topk, device=dev)
     ti = torch.empty(U, topk, device=dev, dtype=torch.int32)
     st = torch.cuda.current_stream().cuda_stream
+    ws = torch.empty(U * 8 * topk * 8, dtype=torch.uint8, device=dev)
+    os.environ["MINER_RK_SPLIT"] = "1"
     libs = {}
     for v in variants:
-        h = ctypes.CDLL(os.path.join(OUT, f"librk_abl{v}.so"))
-        h.miner_rank_topk.argtypes = [P, I, I, P, P, P, I, I, I, I, I, P, P]
+        h = ctypes.CDLL(os.path.join(OUT, f"librk_abl{v.rstrip('s')}.so"))
+        h.miner_rank_topk_ws.argtypes = [P, I, I, P, P, P, I, I, I, I, I, P, P, P]
         libs[v] = h
 
     def launch(v):
-        rc = libs[v].miner_rank_topk(st, 2, 0, mui.data_ptr(), proj.data_ptr(), table.data_ptr(), U, N, d, K, topk,
-                                     ts.data_ptr(), ti.data_ptr())
+        rc = libs[v].miner_rank_topk_ws(st, 2, 0, mui.data_ptr(), proj.data_ptr(), table.data_ptr(), U, N, d, K, topk,
+                                        ts.data_ptr(), ti.data_ptr(), ws.data_ptr() if v.endswith("s") else None)
         assert rc == 0, rc
 
     times = {v: [] for v in variants}
@@ -65,13 +72,13 @@ def run(variants, U=2048, N=200000, reps=3):
     fl = U * N * 4 * K * d
     for v in variants:
         t = statistics.median(times[v])
-        print(f"ABL={v:2d}: {t:8.2f} ms  ({fl / t / 1e9 / 2500:.3f} of fp16 peak)  all {[round(x, 1) for x in times[v]]}",
+        print(f"ABL={v:>3s}: {t:8.2f} ms  ({fl / t / 1e9 / 2500:.3f} of fp16 peak)  all {[round(x, 1) for x in times[v]]}",
               flush=True)
 
 
 if __name__ == "__main__":
     args = sys.argv[1:]
     if args and args[0] == "--build":
-        build([int(a) for a in args[1:]])
+        build(args[1:])
     else:
-        run([int(a) for a in args])
+        run(args)
