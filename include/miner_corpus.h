@@ -65,9 +65,10 @@ int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mu
 
 /*
  * The same with a caller-owned device workspace of miner_rank_topk_workspace_bytes(U, topk) bytes
- * (16-byte aligned; NULL: the form above). With it, on a 256-CU device, the news table is split in
- * 8 slices whose per-user top-k lists are merged by a second launch, and the users are mapped so
- * that the CUs of one XCD share 8 users' rows in their L2. Same results as miner_rank_topk.
+ * (16-byte aligned; NULL: the form above). With it, on a 256-CU device and fewer than 256 users,
+ * the news table is split in 8 slices whose per-user top-k lists are merged by a second launch (8x
+ * the workgroups for small user batches), the users mapped so that the CUs of one XCD share 8
+ * users' rows in their L2. Same results as miner_rank_topk, bit for bit.
  */
 size_t miner_rank_topk_workspace_bytes(int U, int topk);
 int miner_rank_topk_ws(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,

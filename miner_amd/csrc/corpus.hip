@@ -436,8 +436,6 @@ __global__ __launch_bounds__(kThreads) void ue_fused(UeParams p) {
 // ================================================================================================
 constexpr int kUT = 2;            // users per workgroup tile
 constexpr int kNT = 256;          // news per step
-constexpr int kRowB = 128;        // bytes of every image row per d-chunk
-template <class T> constexpr int kEpc = kRowB / (int)sizeof(T);   // elements per chunk
 
 struct RkParams {
   const void* mui;
@@ -476,48 +474,66 @@ __device__ __forceinline__ void rk_dma(uint32_t off, const char* base, unsigned 
                : "=&s"(t) : "v"(off), "s"(base), "s"(m) : "memory");
 }
 
-// image geometry: rows of 128 B, 16-byte chunk c of row `row` at c ^ ((row >> 1) & 7): the 16 rows
-// of a ds_read_b128 lane group (natural or pi order) hit 16 different slots
-__device__ __forceinline__ int rk_swz(int row) { return (row >> 1) & 7; }
+// image geometry: rows of RB bytes per chunk; 16-byte unit c of row `row` at c ^ rk_swz(row) —
+// RB = 128: (row >> 1) & 7, RB = 64: (row >> 2) & 3. Either way the 16 rows of a ds_read_b128 lane
+// group (natural or pi order: lanes {0-3, 12-15, 20-27} read rows {0-3, 12-15, 20-27}) land in 16
+// different 16-byte bank slots.
+template <int RB>
+__device__ __forceinline__ int rk_swz(int row) { return RB == 128 ? (row >> 1) & 7 : (row >> 2) & 3; }
 
-template <class T>
+template <class T, int RB>
 __device__ __forceinline__ void rk_frag(Frag<T>& f, const char* img, int row, int c0) {
 #pragma unroll
   for (int i = 0; i < kNQ<T>; ++i)
-    f.q[i] = *reinterpret_cast<const u32x4*>(img + row * kRowB + (((c0 + i) ^ rk_swz(row)) << 4));
+    f.q[i] = *reinterpret_cast<const u32x4*>(img + row * RB + (((c0 + i) ^ rk_swz<RB>(row)) << 4));
 }
+
+// a wave's vector-memory operations down to N outstanding
+template <int N>
+__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+
+// stream geometry: GEO 0 rows of 128 B, a ring of 2 stages (the next chunk in flight); GEO 1 (16-bit,
+// at least two row tiles per user) rows of 64 B, a ring of 4 stages of the same total size (three
+// chunks in flight)
+template <int GEO> constexpr int kRB = GEO ? 64 : 128;
+template <int GEO> constexpr int kRing = GEO ? 4 : 2;
 
 // total order of ranked entries: higher score first, then lower news id
 __device__ __forceinline__ bool better(float s, int i, float s2, int i2) { return s > s2 || (s == s2 && i < i2); }
 
-template <int NR>
+template <int NR, int GEO = 0>
 struct RkLds {
   static constexpr int kARows = kUT * NR * 32;
-  static constexpr int kStage = (kARows + kNT) * kRowB;
-  static constexpr int kOffList = 2 * kStage;                       // [kUT][kMaxTopk] float + int
-  static constexpr int kOffStage = kOffList + kUT * kMaxTopk * 8;  // staged candidates
-  static constexpr int kOffCnt = kOffStage + kUT * kNT * 8;         // list counts, staged counts
+  static constexpr int kStage = (kARows + kNT) * kRB<GEO>;
+  static constexpr int kOffList = kRing<GEO> * kStage;              // [kUT][kMaxTopk] float + int
+  static constexpr int kOffStage = kOffList + kUT * kMaxTopk * 8;  // staged candidates [2 bufs][kUT][kNT]
+  static constexpr int kOffCnt = kOffStage + 2 * kUT * kNT * 8;     // list counts [kUT], staged [2][kUT]
   static constexpr int kTotal = kOffCnt + 64;
 };
 
-template <class T, int NKT, int SCORE, int NCH = 0, int S = 1>   // NCH: 128-byte d-chunks per row (0: at run time)
+// NCH: RB-byte d-chunks per row (0: at run time); GEO: the stream geometry (kRB / kRing)
+template <class T, int NKT, int SCORE, int NCH = 0, int S = 1, int GEO = 0>
 __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kW = SCORE == MINER_SCORE_WEIGHTED;
   constexpr int NR = kW ? 2 * NKT : NKT;            // row tiles per user: mui (and proj)
-  using LD = RkLds<NR>;
-  constexpr int kChunkSlabs = sizeof(T) == 2 ? 2 : 1;
-  const int d = NCH > 0 ? NCH * kRowB / (int)sizeof(T) : p.d, K = p.K, N = p.N;
-  const int nchunk = NCH > 0 ? NCH : d * (int)sizeof(T) / kRowB;
+  constexpr int RB = kRB<GEO>, RING = kRing<GEO>, PD = RING - 1;   // PD: chunks in flight
+  using LD = RkLds<NR, GEO>;
+  constexpr int kChunkSlabs = RB / (32 * (int)sizeof(T));          // 32-index slabs per chunk
+  static_assert(kChunkSlabs >= 1, "a chunk holds whole slabs");
+  const int d = NCH > 0 ? NCH * RB / (int)sizeof(T) : p.d, K = p.K, N = p.N;
+  const int nchunk = NCH > 0 ? NCH : d * (int)sizeof(T) / RB;
   const int nsteps = ((N + kNT - 1) / kNT + S - 1) / S;            // news steps per slice
   const int ntiles = (p.U + kUT - 1) / kUT;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int uu = wave >> 2, nsub = wave & 3;
   float* list_s = reinterpret_cast<float*>(smem + LD::kOffList);
   int* list_i = reinterpret_cast<int*>(smem + LD::kOffList + kUT * kMaxTopk * 4);
-  float* stg_s = reinterpret_cast<float*>(smem + LD::kOffStage);
-  int* stg_i = reinterpret_cast<int*>(smem + LD::kOffStage + kUT * kNT * 4);
-  int* cnt = reinterpret_cast<int*>(smem + LD::kOffCnt);           // [0,kUT): list sizes, [kUT, 2kUT): staged
+  float* stg_s = reinterpret_cast<float*>(smem + LD::kOffStage);                    // [buf][uu][kNT]
+  int* stg_i = reinterpret_cast<int*>(smem + LD::kOffStage + 2 * kUT * kNT * 4);
+  int* cnt = reinterpret_cast<int*>(smem + LD::kOffCnt);   // [0, kUT) list sizes, kUT + buf * kUT + uu staged
+  // the user's merging wave: 0 and 5 (two SIMDs under the wave -> SIMD w % 4 placement)
+  const bool merger = wave == 5 * uu;
   const T* __restrict__ mui = static_cast<const T*>(p.mui);
   const T* __restrict__ proj = static_cast<const T*>(p.proj);
   const T* __restrict__ news = static_cast<const T*>(p.news);
@@ -534,16 +550,20 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   // the rest news rows (B). The per-lane byte offsets are fixed for the launch (A: within the user's
   // [K, d] array; B: from the step's first news row); the user, step and chunk go into the scalar
   // base of the saddr form. A chunk's blocks are issued spread over the previous chunk's MFMAs.
-  constexpr int kBlk = (LD::kARows + kNT) * kRowB / 1024;          // 1 KiB DMA blocks per stage
+  constexpr int kBlk = (LD::kARows + kNT) * RB / 1024;              // 1 KiB DMA blocks per stage
   static_assert(kBlk % kWaves == 0, "whole DMA blocks per wave");
   constexpr int kJ = kBlk / kWaves;
+  constexpr int kUnits = RB / 16;                                    // 16-byte units per row
+  constexpr int kRpb = 1024 / RB;                                    // rows per DMA block
+  constexpr int kAJ = LD::kARows / (kWaves * kRpb);                  // A blocks per wave (jj < kAJ)
+  static_assert(LD::kARows % (kWaves * kRpb) == 0, "A blocks split evenly over the waves");
   uint32_t voff[kJ];
 #pragma unroll
   for (int jj = 0; jj < kJ; ++jj) {
     const int lane = fresh_lane();
     const int P = (wave + kWaves * jj) * 64 + lane;
-    const int row = P >> 3, cl = (P & 7) ^ rk_swz(row);
-    if (jj < NR) {
+    const int row = P / kUnits, cl = (P % kUnits) ^ rk_swz<RB>(row);
+    if (jj < kAJ) {
       const int k = min(32 * (((row >> 5) % NR) % NKT) + (row & 31), K - 1);
       voff[jj] = (uint32_t)(k * d) * (uint32_t)sizeof(T) + cl * 16;
     } else {
@@ -554,22 +574,22 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
   int nti = first, nsl = 0, nc = 0;
   auto dma_block = [&](int jj, int stage) {
     const unsigned la = __builtin_amdgcn_readfirstlane(lds_offset(smem + stage * LD::kStage + (wave + kWaves * jj) * 1024));
-    if (jj < NR) {
-      const int row0 = 8 * wave + 64 * jj;
+    if (jj < kAJ) {
+      const int row0 = (wave + kWaves * jj) * kRpb;
       const int t = (row0 >> 5) % NR, ou = row0 / (NR * 32);
       const int user = min(nti * kUT + ou, p.U - 1);
       const T* src = (kW && t >= NKT) ? proj : mui;
-      rk_dma(voff[jj], reinterpret_cast<const char*>(src + (size_t)user * K * d) + nc * kRowB, la);
+      rk_dma(voff[jj], reinterpret_cast<const char*>(src + (size_t)user * K * d) + nc * RB, la);
     } else {
       const int st = news_step(nsl);
       if (st * kNT + kNT <= N) {
-        rk_dma(voff[jj], reinterpret_cast<const char*>(news + (size_t)st * kNT * d) + nc * kRowB, la);
+        rk_dma(voff[jj], reinterpret_cast<const char*>(news + (size_t)st * kNT * d) + nc * RB, la);
       } else {                           // the table's last (partial) step: rows clamped to N - 1
         const int lane = fresh_lane();
         const int P = (wave + kWaves * jj) * 64 + lane;
-        const int row = P >> 3, cl = (P & 7) ^ rk_swz(row);
+        const int row = P / kUnits, cl = (P % kUnits) ^ rk_swz<RB>(row);
         const int n = min(st * kNT + (row - LD::kARows), N - 1);
-        dma_b128_rt(news + (size_t)n * d + nc * kEpc<T> + cl * (16 / (int)sizeof(T)), la);
+        dma_b128_rt(news + (size_t)n * d + nc * (RB / (int)sizeof(T)) + cl * (16 / (int)sizeof(T)), la);
       }
     }
   };
@@ -580,12 +600,82 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
     }
   };
 
-  if (threadIdx.x < 2 * kUT) cnt[threadIdx.x] = 0;
-  if (!(MINER_RK_ABL & 1)) {
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);   // static priority for the second half (-0.8 %)
+  if (threadIdx.x < 3 * kUT) cnt[threadIdx.x] = 0;
+
+  // merge the candidates staged in buffer `buf` into user uu's running top-k (one wave). The list
+  // (best first) and the staged entries are ranked in parallel: an entry's new position is the
+  // number of entries of both sets better than it (a total order on distinct news ids); entries
+  // ranked past topk drop out. Every LDS read comes before the first write (one wave, in order).
+  auto merge = [&](int buf) {
+    const int ns = cnt[kUT + buf * kUT + uu];
+    if (ns == 0) return;
+    const int lane = fresh_lane();
+    const int c = cnt[uu];
+    float* ls = list_s + uu * kMaxTopk;
+    int* li = list_i + uu * kMaxTopk;
+    const float* ss = stg_s + (buf * kUT + uu) * kNT;
+    const int* si = stg_i + (buf * kUT + uu) * kNT;
+    constexpr int kLT = kMaxTopk / 64, kST = kNT / 64;
+    float lv[kLT], sv[kST];
+    int lid[kLT], sid[kST], lr[kLT], sr[kST];
 #pragma unroll
-    for (int jj = 0; jj < kJ; ++jj) dma_block(jj, 0);
+    for (int t = 0; t < kLT; ++t) {
+      const int i = min(lane + 64 * t, kMaxTopk - 1);
+      lv[t] = ls[i];
+      lid[t] = li[i];
+      lr[t] = lane + 64 * t;
+    }
+#pragma unroll
+    for (int v = 0; v < kST; ++v) {
+      const int j = min(lane + 64 * v, kNT - 1);
+      sv[v] = ss[j];
+      sid[v] = si[j];
+      sr[v] = 0;
+    }
+    for (int j2 = 0; j2 < ns; ++j2) {
+      const float s2 = ss[j2];
+      const int i2 = si[j2];
+      int nl = 0;                              // list entries better than staged entry j2
+#pragma unroll
+      for (int t = 0; t < kLT; ++t) {
+        lr[t] += better(s2, i2, lv[t], lid[t]) ? 1 : 0;   // staged entries better than each entry
+        nl += __popcll(__ballot(lane + 64 * t < c && better(lv[t], lid[t], s2, i2)));
+      }
+#pragma unroll
+      for (int v = 0; v < kST; ++v) {
+        sr[v] += better(s2, i2, sv[v], sid[v]) ? 1 : 0;
+        if (j2 == lane + 64 * v) sr[v] += nl;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < kLT; ++t) {
+      if (lane + 64 * t < c && lr[t] < p.topk) {
+        ls[lr[t]] = lv[t];
+        li[lr[t]] = lid[t];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < kST; ++v) {
+      if (lane + 64 * v < ns && sr[v] < p.topk) {
+        ls[sr[v]] = sv[v];
+        li[sr[v]] = sid[v];
+      }
+    }
+    if (lane == 0) {
+      cnt[uu] = min(c + ns, p.topk);
+      cnt[kUT + buf * kUT + uu] = 0;
+    }
+  };
+
+  for (int q0 = 0; q0 < PD && q0 < total_chunks; ++q0) {   // prologue: the first PD chunks
+    if (!(MINER_RK_ABL & 1)) {
+#pragma unroll
+      for (int jj = 0; jj < kJ; ++jj) dma_block(jj, q0);
+    }
+    advance();
   }
-  advance();
   int q = 0;
   for (int ti = first; ti < ntiles; ti += tstride) {
     for (int sl = 0; sl < nsteps; ++sl) {
@@ -594,24 +684,32 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
 #pragma unroll
       for (int t = 0; t < NR; ++t) { acc[t][0] = zero16(); acc[t][1] = zero16(); }
       for (int c = 0; c < nchunk; ++c, ++q) {
-        if (!(MINER_RK_ABL & 1)) vm_wait_all();
-        if (!(MINER_RK_ABL & 8)) __syncthreads();        // chunk q landed; chunk q - 1's stage is free
-        const bool pre = !(MINER_RK_ABL & 1) && q + 1 < total_chunks;
+        // chunk q landed (this wave's DMAs of chunks q + 1 .. q + PD - 1 may stay in flight), then
+        // for every wave; chunk q - 1's stage is free
+        if (!(MINER_RK_ABL & 1)) {
+          if (PD > 1 && q + PD - 1 < total_chunks) vm_wait_n<(PD - 1) * kJ>();
+          else vm_wait_all();
+        }
+        if (!(MINER_RK_ABL & 8)) __syncthreads();
+        // the previous step's staged candidates (its epilogue is behind this barrier); the next
+        // epilogue reads the list only after this chunk's barriers
+        if (c == 0 && sl > 0 && merger && !(MINER_RK_ABL & 4)) merge((sl - 1) & 1);
+        const bool pre = !(MINER_RK_ABL & 1) && q + PD < total_chunks;
         const int lane = fresh_lane();
         const int r = lane & 31, h = lane >> 5;
-        const char* img = smem + (q & 1) * LD::kStage;
-        const char* bimg = img + LD::kARows * kRowB;
+        const char* img = smem + (q % RING) * LD::kStage;
+        const char* bimg = img + LD::kARows * RB;
         constexpr int kPairs = kChunkSlabs * NR;
 #pragma unroll
         for (int s = 0; s < kChunkSlabs; ++s) {
-          const int c0 = sizeof(T) == 2 ? 4 * s + 2 * h : 4 * h;
+          const int c0 = (2 * s + h) * kNQ<T>;
           Frag<T> bf[2];
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) rk_frag<T>(bf[nt], bimg, 64 * nsub + 32 * nt + r, c0);
+          for (int nt = 0; nt < 2; ++nt) rk_frag<T, RB>(bf[nt], bimg, 64 * nsub + 32 * nt + r, c0);
 #pragma unroll
           for (int t = 0; t < NR; ++t) {
             Frag<T> af;
-            rk_frag<T>(af, img, (uu * NR + t) * 32 + pi_row(r), c0);
+            rk_frag<T, RB>(af, img, (uu * NR + t) * 32 + pi_row(r), c0);
             if (!(MINER_RK_ABL & 2)) {
               mma_slab<T>(acc[t][0], af, bf[0]);
               mma_slab<T>(acc[t][1], af, bf[1]);
@@ -623,11 +721,12 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
             constexpr int kWin = MINER_RK_DMAW < kPairs ? MINER_RK_DMAW : kPairs;
 #pragma unroll
             for (int jj = 0; jj < kJ; ++jj)
-              if (jj * kWin / kJ == s * NR + t && pre) dma_block(jj, (q + 1) & 1);
+              if (jj * kWin / kJ == s * NR + t && pre) dma_block(jj, (q + PD) % RING);
           }
         }
         if (pre) advance();
       }
+      if (nchunk == 1 && sl > 0) __syncthreads();   // (one chunk per step: the merge above is done)
       // ---- epilogue: click score of (user uu, news) for this wave's 64 news ----
       if (MINER_RK_ABL & 4) {            // every accumulator stays live (no MFMA is dead code)
         float z = 0.f;
@@ -655,14 +754,18 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
                 if (32 * kt + 16 * h + e < K) mx = fmaxf(mx, acc[NKT + kt][nt][e]);
             mx = xor32_max(mx);
             float s0 = 0.f, s1 = 0.f;
+            // 16-bit: exp(x - mx) as exp2(x·log2 e - mx·log2 e), one fma + v_exp_f32 per interest
+            const float mxl = mx * 1.44269504088896340736f;
 #pragma unroll
             for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
               for (int e = 0; e < 16; ++e)
                 if (32 * kt + 16 * h + e < K) {
-                  const float ex = cx_exp<T>(acc[NKT + kt][nt][e] - mx);
+                  const float lg = acc[NKT + kt][nt][e];
+                  const float ex = sizeof(T) == 2 ? __builtin_amdgcn_exp2f(__builtin_fmaf(lg, 1.44269504088896340736f, -mxl))
+                                                  : expf(lg - mx);
                   s0 += ex;
-                  s1 += ex * acc[kt][nt][e];
+                  s1 = __builtin_fmaf(ex, acc[kt][nt][e], s1);
                 }
             score = xor32_sum(s1) / xor32_sum(s0);       // Σ softmax_k(Lg) · M  (model.py:213-214)
           } else if constexpr (SCORE == MINER_SCORE_MAX) {
@@ -685,66 +788,28 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
           const bool cand = h == 0 && n < N && user < p.U && better(score, n, th_s, th_i);
           const unsigned long long bal = __ballot(cand);
           if (bal) {
+            const int buf = sl & 1;
             int b0 = 0;
-            if (lane == 0) b0 = atomicAdd(&cnt[kUT + uu], __popcll(bal));
+            if (lane == 0) b0 = atomicAdd(&cnt[kUT + buf * kUT + uu], __popcll(bal));
             b0 = __builtin_amdgcn_readfirstlane(b0);
             if (cand) {
               const int slot = b0 + __popcll(bal & ((1ull << lane) - 1));
-              stg_s[uu * kNT + slot] = score;
-              stg_i[uu * kNT + slot] = n;
+              stg_s[(buf * kUT + uu) * kNT + slot] = score;
+              stg_i[(buf * kUT + uu) * kNT + slot] = n;
             }
           }
         }
       }
-      __syncthreads();
-      // ---- merge the staged candidates into the running top-k (one wave per user) ----
-      if (nsub == 0) {
-        const int lane = fresh_lane();
-        const int ns_ = cnt[kUT + uu];
-        float* ls = list_s + uu * kMaxTopk;
-        int* li = list_i + uu * kMaxTopk;
-        int c = cnt[uu];
-        for (int j = 0; j < ns_; ++j) {
-          const float s = stg_s[uu * kNT + j];
-          const int id = stg_i[uu * kNT + j];
-          if (c == p.topk && !better(s, id, ls[p.topk - 1], li[p.topk - 1])) continue;
-          // insertion point: entries better than the candidate
-          int pos = 0;
-          float vs[kMaxTopk / 64];
-          int vi[kMaxTopk / 64];
-#pragma unroll
-          for (int t = 0; t < kMaxTopk / 64; ++t) {
-            const int i = lane + 64 * t;
-            vs[t] = ls[i];
-            vi[t] = li[i];
-            pos += __popcll(__ballot(i < c && better(vs[t], vi[t], s, id)));
-          }
-          // shift [pos, min(c, topk - 1)) up by one, then insert
-#pragma unroll
-          for (int t = 0; t < kMaxTopk / 64; ++t) {
-            const int i = lane + 64 * t;
-            if (i >= pos && i < c && i + 1 < p.topk) {
-              ls[i + 1] = vs[t];
-              li[i + 1] = vi[t];
-            }
-          }
-          if (lane == 0) {
-            ls[pos] = s;
-            li[pos] = id;
-          }
-          c = min(c + 1, p.topk);
-        }
-        if (lane == 0) {
-          cnt[uu] = c;
-          cnt[kUT + uu] = 0;
-        }
-      }
-      __syncthreads();
+      // the staged candidates are merged at the next step's first chunk (merge, above), the last
+      // step's below
     }
-    // ---- this tile's users are done: write their top-k ----
+    // ---- this tile's users are done: merge the last step, write their top-k ----
     {
+      __syncthreads();
+      if (merger && !(MINER_RK_ABL & 4)) merge((nsteps - 1) & 1);
+      __syncthreads();
       const int user = ti * kUT + uu;
-      if (nsub == 0 && user < p.U) {
+      if (merger && user < p.U) {
         const int lane = fresh_lane();
         const size_t o = ((size_t)user * S + slice) * p.topk;
         float* ds = S == 1 ? p.top_s : p.ws_s;
@@ -843,25 +908,31 @@ int ue_dispatch(void* stream, const UeParams& prm) {
   return g ? ue_launch<T, 2, true>(stream, prm) : ue_launch<T, 2, false>(stream, prm);
 }
 
-// the split form (S = kSplit news slices, rk_merge) when the caller gave a workspace and the device
-// has the 256 CUs its tile-to-XCD map assumes (MINER_RK_SPLIT=0: the unsplit form for A/B)
+// the split form (S = kSplit news slices, rk_merge) when the caller gave a workspace, the device has
+// the 256 CUs its tile-to-XCD map assumes, and the users are too few to fill the CUs with 2-user
+// tiles (< 256 users): at U = 2,048 it measured 90.5 vs 85.9 ms per config-5 step (each slice's
+// top-k warms up on its own; its L2 hit rate is higher, 69 vs 45 %, but the stream is not what
+// bounds it). MINER_RK_SPLIT=1 / 0 forces either form.
 bool rk_split(const RkParams& prm) {
+  if (prm.ws_s == nullptr || prm.ws_i == nullptr || num_cus() != 256) return false;
   const char* ev = getenv("MINER_RK_SPLIT");
-  const bool on = ev && ev[0] == '1';
-  return prm.ws_s != nullptr && prm.ws_i != nullptr && num_cus() == 256 && on;
+  if (ev && (ev[0] == '0' || ev[0] == '1')) return ev[0] == '1';
+  return (prm.U + kUT - 1) / kUT < num_cus();
 }
 
-template <class T, int NKT, int S>
-int rk_launch(void* stream, const RkParams& prm) {
+template <class T, int NKT, int S, int GEO>
+int rk_launch_geo(void* stream, const RkParams& prm, bool split) {
   // d = 768 in 16-bit (config 5): the chunk count compile-time (MINER_RK_NCH_RT: the run-time form)
-  const bool split = rk_split(prm);
-  void (*kern)(RkParams) = split ? rk_fused<T, NKT, S, 0, kSplit> : rk_fused<T, NKT, S>;
+  void (*kern)(RkParams) = split ? rk_fused<T, NKT, S, 0, kSplit, GEO> : rk_fused<T, NKT, S, 0, 1, GEO>;
   if constexpr (sizeof(T) == 2) {
     // (a compile-time K = 64 as well measured 3.9 % faster but not bit-identical top-k: not used)
-    if (prm.d == 768 && !getenv("MINER_RK_NCH_RT")) kern = split ? rk_fused<T, NKT, S, 12, kSplit> : rk_fused<T, NKT, S, 12>;
+    constexpr int kN768 = 768 * 2 / kRB<GEO>;
+    if (prm.d == 768 && !getenv("MINER_RK_NCH_RT"))
+      kern = split ? rk_fused<T, NKT, S, kN768, kSplit, GEO> : rk_fused<T, NKT, S, kN768, 1, GEO>;
   }
   constexpr int NR = S == MINER_SCORE_WEIGHTED ? 2 * NKT : NKT;
-  const int lds = RkLds<NR>::kTotal;
+  const int lds = RkLds<NR, GEO>::kTotal;
+  static_assert(RkLds<NR, GEO>::kTotal <= 160 * 1024, "ranker LDS");
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   const int ntiles = (prm.U + kUT - 1) / kUT;
@@ -875,6 +946,14 @@ int rk_launch(void* stream, const RkParams& prm) {
                      prm.ws_i, prm.U, prm.topk, prm.top_s, prm.top_i);
   e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+template <class T, int NKT, int S>
+int rk_launch(void* stream, const RkParams& prm) {
+  const bool split = rk_split(prm);
+  // (GEO 1 — 64-byte rows through a 4-stage ring, three chunks in flight instead of one — measured
+  // slower: 95.9 vs 89.7 ms per config-5 step, twice the barriers for no gain in the gather rate)
+  return rk_launch_geo<T, NKT, S, 0>(stream, prm, split);
 }
 
 template <class T>

@@ -160,7 +160,8 @@ struct FfParams {
   float* scores;             // [sum C_b] or null
   float* user_out;           // [B, 256] or null
   int B, L, C, n_news;
-  int abl;                   // experiment bits (MINER_FF_ABL): 1 = static priority for waves 4-7
+  int abl;                   // experiment bits (MINER_FF_ABL): 1 = static priority for waves 4-7,
+                             // 2 = history rows DMA'd with the default cache policy instead of nt
 };
 
 // LDS carve (bytes): two activation images | LN / pooler exchange | head softmax weights | user
@@ -488,7 +489,7 @@ __device__ __forceinline__ void history_rows(const FfParams& p, int bn, int wave
   }
 }
 template <class T>
-__device__ __forceinline__ void dma_history(const T* base, const int (&rows)[kHistIds<T>], char* img, int wave) {
+__device__ __forceinline__ void dma_history(const T* base, const int (&rows)[kHistIds<T>], char* img, int wave, bool rt) {
   const int lane = fresh_lane();
 #pragma unroll
   for (int k = 0; k < kDmaPerWave<T>; ++k) {
@@ -496,7 +497,9 @@ __device__ __forceinline__ void dma_history(const T* base, const int (&rows)[kHi
     const int m = P / kCpr<T>, pc = P % kCpr<T>;
     const int row = kRowsPerDma<T> == 2 ? ((lane >> 5) ? rows[2 * k + 1] : rows[2 * k]) : rows[k];
     const T* g = base + (size_t)row * kH + ((pc ^ (m & 15)) << 4) / (int)sizeof(T);
-    dma_b128(g, __builtin_amdgcn_readfirstlane(lds_offset(img + (wave + kWaves * k) * 1024)));
+    const unsigned la = __builtin_amdgcn_readfirstlane(lds_offset(img + (wave + kWaves * k) * 1024));
+    if (rt) dma_b128_rt(g, la);
+    else dma_b128(g, la);
   }
 }
 
@@ -613,7 +616,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
   if (blockIdx.x < p.B) {
     int rows[kHistIds<T>];
     history_rows<T, GATHER>(p, blockIdx.x, wave, rows);
-    dma_history<T>(hist, rows, img1, wave);
+    dma_history<T>(hist, rows, img1, wave, (p.abl & 2) != 0);
     mraw = load_mask(p, blockIdx.x);
   }
 
@@ -807,7 +810,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
     load_pos();
     if (has_next) mraw = load_mask(p, bn);
     // next impression's history rows -> img1 (free until the next impression starts)
-    if (has_next) dma_history<T>(hist, rows_next, img1, wave);
+    if (has_next) dma_history<T>(hist, rows_next, img1, wave, (p.abl & 2) != 0);
 
     // candidate rows of this impression, in flight during the pooler
     typename CandVec<T>::type cv[kCandPf];

@@ -150,3 +150,19 @@ def test_split_equals_unsplit(dtype, U, N, topk, monkeypatch):
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), st
         if N < topk:
             assert (a[1][:, N:] == -1).all()
+
+
+@pytest.mark.parametrize("K", [64, 32])
+@pytest.mark.parametrize("score_type", ["weighted", "max", "mean"])
+def test_16bit_one_chunk_rows(K, score_type):
+    """d = 64 in 16-bit: one d-chunk per news step, so the deferred top-k merge of a step meets the
+    next step's epilogue with no chunk barrier in between (corpus.hip adds one) — against the oracle."""
+    gen = torch.Generator().manual_seed(K + len(score_type))
+    U, d, N = 9, 64, 700
+    mui = torch.randn(U, K, d, generator=gen) / 2
+    proj = torch.randn(U, K, d, generator=gen) / 2
+    table = torch.randn(N, d, generator=gen) / d ** 0.5
+    m16, p16, t16 = (x.to(DEV, torch.float16) for x in (mui, proj, table))
+    ts, ti = corpus.rank_topk(m16, p16, t16, 50, score_type=score_type)
+    ref = co.corpus_scores(m16.float().cpu(), p16.float().cpu(), t16.float().cpu(), score_type)
+    check_topk(ts, ti, ref.double().numpy(), 50, RANK16_TOL)

@@ -4,7 +4,8 @@ every build timed interleaved in one process on the same inputs (2048 users x 20
 
     python tools/rk_ablate.py --build 0 1 2 4 5 6 7 8     # CPU: tools/bisect/librk_abl<bits>.so
     python tools/rk_ablate.py 0 1 2 4 5 6 7 8 16s          # GPU; a trailing "s": the split form
-                                                           # (miner_rank_topk_ws, MINER_RK_SPLIT=1)
+                                                           # (miner_rank_topk_ws, MINER_RK_SPLIT=1);
+                                                           # "g": the 64-byte 4-stage geometry
 """
 import ctypes
 import os
@@ -48,11 +49,12 @@ def run(variants, U=2048, N=200000, reps=3):
     os.environ["MINER_RK_SPLIT"] = "1"
     libs = {}
     for v in variants:
-        h = ctypes.CDLL(os.path.join(OUT, f"librk_abl{v.rstrip('s')}.so"))
+        h = ctypes.CDLL(os.path.join(OUT, f"librk_abl{v.rstrip('sg')}.so"))
         h.miner_rank_topk_ws.argtypes = [P, I, I, P, P, P, I, I, I, I, I, P, P, P]
         libs[v] = h
 
     def launch(v):
+        os.environ["MINER_RK_GEO"] = "1" if "g" in v else "0"
         rc = libs[v].miner_rank_topk_ws(st, 2, 0, mui.data_ptr(), proj.data_ptr(), table.data_ptr(), U, N, d, K, topk,
                                         ts.data_ptr(), ti.data_ptr(), ws.data_ptr() if v.endswith("s") else None)
         assert rc == 0, rc
