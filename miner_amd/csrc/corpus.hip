@@ -952,7 +952,12 @@ template <class T, int NKT, int S>
 int rk_launch(void* stream, const RkParams& prm) {
   const bool split = rk_split(prm);
   // (GEO 1 — 64-byte rows through a 4-stage ring, three chunks in flight instead of one — measured
-  // slower: 95.9 vs 89.7 ms per config-5 step, twice the barriers for no gain in the gather rate)
+  // slower: 95.9 vs 89.7 ms per config-5 step, twice the barriers for no gain in the gather rate;
+  // diagnostic builds with -DMINER_RK_GEO1 launch it)
+#ifdef MINER_RK_GEO1
+  constexpr int NR = S == MINER_SCORE_WEIGHTED ? 2 * NKT : NKT;
+  if constexpr (sizeof(T) == 2 && NR >= 2) return rk_launch_geo<T, NKT, S, 1>(stream, prm, split);
+#endif
   return rk_launch_geo<T, NKT, S, 0>(stream, prm, split);
 }
 
