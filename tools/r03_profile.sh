@@ -32,11 +32,11 @@ run_passes bf16 bf16 "$B" 768 104000 5
 run_passes c2x2 fp32 50000 256 65238 3
 run_passes c2bf16 bf16 50000 256 65238 3
 P="$R/tools/pmc_traffic.py"
-python3 "$P" --batch "$B" --tag news_score_x2ILi0ELb0ELi12ELi2E --tag "news_score_x2<0, false, 12, 2>" \
+python3 "$P" --batch "$B" --tag "news_score_x2<0, false, 12, 2, false>" \
   --workload news_L50_K32_d768_C40_N104000_fp32 --kernel-name "news_score_x2<weighted,dense,12,MIND>" \
   --out "$R/profiles/pmc_traffic_news_x2.json" "$O"/x2_p* > "$O/traffic_x2.txt"
 python3 "$P" --batch "$B" --news "$O"/bf16_p* > "$O/traffic_bf16.txt"
-python3 "$P" --batch 50000 --tag news_score_x2ILi0ELb0ELi4ELi2E --tag "news_score_x2<0, false, 4, 2>" \
+python3 "$P" --batch 50000 --tag "news_score_x2<0, false, 4, 2, false>" \
   --workload news_L50_K32_d256_C40_N65238_fp32 --kernel-name "news_score_x2<weighted,dense,4,MIND>" \
   --out "$R/profiles/pmc_traffic_news_c2_x2.json" "$O"/c2x2_p* > "$O/traffic_c2x2.txt"
 python3 "$P" --batch 50000 --tag news_scoreIDF16bLi0ELb0ELi3ELi64ELi4ELi1E --tag "news_score<__bf16, 0, false, 3, 64, 4, 1>" \
