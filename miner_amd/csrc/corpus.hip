@@ -746,14 +746,15 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
           const int n = st * kNT + 64 * nsub + 32 * nt + r;
           float score;
           if constexpr (kW) {
-            float mx = -INFINITY;
+            // 4 independent max / sum chains per lane (a 32-long dependent chain each otherwise)
+            float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
             for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
               for (int e = 0; e < 16; ++e)
-                if (32 * kt + 16 * h + e < K) mx = fmaxf(mx, acc[NKT + kt][nt][e]);
-            mx = xor32_max(mx);
-            float s0 = 0.f, s1 = 0.f;
+                if (32 * kt + 16 * h + e < K) m4[e & 3] = fmaxf(m4[e & 3], acc[NKT + kt][nt][e]);
+            const float mx = xor32_max(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+            float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
             // 16-bit: exp(x - mx) as exp2(x·log2 e - mx·log2 e), one fma + v_exp_f32 per interest
             const float mxl = mx * 1.44269504088896340736f;
 #pragma unroll
@@ -764,10 +765,11 @@ __global__ __launch_bounds__(kThreads) void rk_fused(RkParams p) {
                   const float lg = acc[NKT + kt][nt][e];
                   const float ex = sizeof(T) == 2 ? __builtin_amdgcn_exp2f(__builtin_fmaf(lg, 1.44269504088896340736f, -mxl))
                                                   : expf(lg - mx);
-                  s0 += ex;
-                  s1 = __builtin_fmaf(ex, acc[kt][nt][e], s1);
+                  s0[e & 3] += ex;
+                  s1[e & 3] = __builtin_fmaf(ex, acc[kt][nt][e], s1[e & 3]);
                 }
-            score = xor32_sum(s1) / xor32_sum(s0);       // Σ softmax_k(Lg) · M  (model.py:213-214)
+            const float t0 = (s0[0] + s0[1]) + (s0[2] + s0[3]), t1 = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+            score = xor32_sum(t1) / xor32_sum(t0);       // Σ softmax_k(Lg) · M  (model.py:213-214)
           } else if constexpr (SCORE == MINER_SCORE_MAX) {
             float mx = -INFINITY;
 #pragma unroll
