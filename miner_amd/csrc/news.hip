@@ -1049,6 +1049,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   // chunks ahead, then the X / mui slab and the candidate product of this chunk.
   // `mode`: 1 X, 2 candidate product, 4 mui out
   NS_STAMP_DECL
+  // the item's history groups fit one 32-slot slab (<= 32 groups: the left padding is one group):
+  // the second slab's attention weights are all 0, its transposed reads and MFMAs are skipped
+  bool one_slab = false;
   auto chunk = [&](int ci, int cc, int mode, int ncand, const uint32_t* iH, const uint32_t* iC, unsigned iLv,
                    int ich) {
     NS_STAMP(2);
@@ -1062,6 +1065,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       f32x16 ax = zero16();
 #pragma unroll
       for (int ls = 0; ls < 2; ++ls) {
+        if (ls == 1 && one_slab) break;
         Frag<T> ef;
         if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -1112,6 +1116,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
     int c_off, c_cnt;
     cands(ci, c_off, c_cnt);
     const int cn = max(1, (c_cnt + 63) >> 6);
+    one_slab = __builtin_amdgcn_readfirstlane(grp_u(smem, ci & 3)[0]) <= 32;
     for (int cp = 0; cp < cn; ++cp) {
       const int cntp = min(64, c_cnt - 64 * cp);
       const bool need_c = WITH_CAND && (ct == 0 || cntp > 32) && (P == 0 || WEIGHTED);
