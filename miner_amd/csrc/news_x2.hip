@@ -864,7 +864,16 @@ int x2_launch(void* stream, const X2Params& prm) {
       case MINER_SCORE_NONE: kern = news_score_x2<MINER_SCORE_NONE, false, NCHV, 0, true>; break;             \
       default: kern = rg ? news_score_x2<MINER_SCORE_MAX, true, NCHV, 0, true> : news_score_x2<MINER_SCORE_MAX, false, NCHV, 0, true>; break; \
     }
-    if (prm.d == 768) { X2_PICKL(12) } else { X2_PICKL(0) }
+    // the MIND shape with no bias and no mui output (the reference's default eval) compile-time, as
+    // the plain-scoring form below
+    const bool plainl = prm.L == 50 && prm.K == 32 && !prm.bias && !prm.mui_out &&
+                        prm.score_type == MINER_SCORE_WEIGHTED && !getenv("MINER_NEWS_SHP_RT");
+    if (prm.d == 768) {
+      if (plainl) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 12, 2, true> : news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2, true>;
+      else { X2_PICKL(12) }
+    } else {
+      X2_PICKL(0)
+    }
 #undef X2_PICKL
   } else {
 #define X2_PICK(NCHV)                                                                                        \

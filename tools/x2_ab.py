@@ -3,7 +3,7 @@ extra flags, each built alone): the same precomputed tables and impressions (con
 bench's synthetic ids), median ms per launch and max |score difference| against the first build.
 
     python tools/x2_ab.py --build NAME [REV|-] [FLAGS...]   # CPU: tools/bisect/libx2_NAME.so
-    python tools/x2_ab.py NAME1 NAME2 ... [--B N]          # GPU
+    python tools/x2_ab.py NAME1 NAME2 ... [--B N]          # GPU (X2AB_LOSS=1: with the disagreement)
 """
 import ctypes
 import os
@@ -54,13 +54,15 @@ def run(names, B=1_000_000, reps=5):
         h.miner_score_news_x2.argtypes = [P, I, P, P, P, P, P, I, P, P, P, P, P, I, I, I, I, I, P, P, P]
         libs[n] = h
     out = {n: torch.empty(B * C, device=dev) for n in names}
+    loss = os.environ.get("X2AB_LOSS") == "1"          # with the eval loss's disagreement output
+    dis = {n: torch.empty(B, device=dev) for n in names} if loss else None
 
     def launch(n):
         px = nt.x2
         rc = libs[n].miner_score_news_x2(st, 0, px.table2.data_ptr(), px.table_ws.data_ptr(), nt.logits.data_ptr(),
                                          px.proj2.data_ptr(), px.proj_ws.data_ptr(), n_news, beh.his_ids.data_ptr(),
                                          mask.data_ptr(), None, beh.cand_ids.data_ptr(), None, B, L, C, d, K,
-                                         out[n].data_ptr(), None, None)
+                                         out[n].data_ptr(), None, dis[n].data_ptr() if loss else None)
         assert rc == 0, rc
 
     times = {n: [] for n in names}
@@ -77,6 +79,8 @@ def run(names, B=1_000_000, reps=5):
             times[n].append(a.elapsed_time(b))
     for n in names:
         diff = float((out[n] - out[names[0]]).abs().max())
+        if loss:
+            diff = max(diff, float((dis[n] - dis[names[0]]).abs().max()))
         t = statistics.median(times[n])
         print(f"{n}: {t:.3f} ms per {B} impressions ({B * C / t / 1e3:.1f} M pairs/s), all "
               f"{[round(x, 2) for x in times[n]]}, max |diff vs {names[0]}| {diff:.2e}", flush=True)
