@@ -871,6 +871,8 @@ int x2_launch(void* stream, const X2Params& prm) {
     if (prm.d == 768) {
       if (plainl) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 12, 2, true> : news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2, true>;
       else { X2_PICKL(12) }
+    } else if (prm.d == 256 && plainl) {   // config 2 (MIND-small)
+      kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 4, 2, true> : news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2, true>;
     } else {
       X2_PICKL(0)
     }

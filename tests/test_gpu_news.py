@@ -310,6 +310,7 @@ def test_bad_inputs_raise():
 
 @pytest.mark.parametrize("B,L,d,C,K,ragged", [
     (300, 50, 768, 40, 32, None),      # config 3 shape
+    (700, 50, 256, 40, 32, None),      # config 2 shape (compile-time d = 256 form)
     (257, 20, 64, 5, 4, None),         # config 1 shape: one chunk per row, K = 4
     (90, 64, 128, 33, 16, None),       # L = 64, K = 16 (interest tile 1 empty)
     (40, 37, 320, 150, 12, None),      # three candidate passes
