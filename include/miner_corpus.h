@@ -65,10 +65,12 @@ int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mu
 
 /*
  * The same with a caller-owned device workspace of miner_rank_topk_workspace_bytes(U, topk) bytes
- * (16-byte aligned; NULL: the form above). With it, on a 256-CU device and fewer than 256 users,
- * the news table is split in 8 slices whose per-user top-k lists are merged by a second launch (8x
- * the workgroups for small user batches), the users mapped so that the CUs of one XCD share 8
- * users' rows in their L2. Same results as miner_rank_topk, bit for bit.
+ * (16-byte aligned; NULL: the form above). With it, on a 256-CU device and fewer than 256 two-user
+ * tiles (U <= 510; MINER_RK_SPLIT=1 / 0 forces either form), the news table is split in 8 slices
+ * whose per-user top-k lists are merged by a second launch (8x the workgroups for small user
+ * batches), the users mapped so that the CUs of one XCD share 8 users' rows in their L2. Same
+ * results as miner_rank_topk, bit for bit. miner_rank_topk_workspace_bytes returns 0 when the split
+ * form would not run (larger U), so no workspace need be allocated then.
  */
 size_t miner_rank_topk_workspace_bytes(int U, int topk);
 int miner_rank_topk_ws(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,

@@ -41,8 +41,9 @@ int miner_impression_metrics(void* stream, const float* scores, const uint8_t* l
 /*
  * The flattened global `auc` of the reference (src/evaluation.py:53-55: sklearn roc_auc_score over
  * every (label, probability) pair of the eval set), exactly, on the device: a radix sort of the
- * scores (hipCUB), a reduce-by-key over runs of equal scores and an integer Mann-Whitney sum with
- * ties counted 1/2.  n <= 2^31 - 1 pairs; `scores` fp32, `labels` uint8 0/1 (device memory);
+ * scores (rocPRIM), a reduce-by-key over runs of equal scores and an integer Mann-Whitney sum with
+ * ties counted 1/2.  n (int64_t) <= 2^31 - 1 pairs, MINER_ESHAPE past it (the rocPRIM sort's
+ * 32-bit sizes); `scores` fp32, `labels` uint8 0/1 (device memory);
  * `workspace` caller-owned device memory of at least miner_auc_workspace_bytes(n) bytes (about
  * 33 bytes per pair); `auc_out` one float64 in DEVICE memory, NaN when one class is absent
  * (sklearn raises there).

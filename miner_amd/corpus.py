@@ -127,7 +127,10 @@ def rank_topk(user_mui: Tensor, user_proj: Optional[Tensor], news: Tensor, topk:
     dev = mui.device
     top_s = torch.empty(U, topk, dtype=torch.float32, device=dev)
     top_i = torch.empty(U, topk, dtype=torch.int32, device=dev)
-    ws = torch.empty(int(_lib.lib().miner_rank_topk_workspace_bytes(U, topk)), dtype=torch.uint8, device=dev)
+    # a workspace only when the split form will run (U <= 510 on a 256-CU device, or MINER_RK_SPLIT=1):
+    # 0 bytes otherwise, and the kernel then takes the unsplit form
+    nws = int(_lib.lib().miner_rank_topk_workspace_bytes(U, topk))
+    ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws else None
     with torch.cuda.device(dev):
         rc = _lib.lib().miner_rank_topk_ws(_stream(dev), dt, st, _ptr(mui), _ptr(proj), _ptr(tab), U, N, d, K, topk,
                                            _ptr(top_s), _ptr(top_i), _ptr(ws))

@@ -912,14 +912,19 @@ int ue_dispatch(void* stream, const UeParams& prm) {
 
 // the split form (S = kSplit news slices, rk_merge) when the caller gave a workspace, the device has
 // the 256 CUs its tile-to-XCD map assumes, and the users are too few to fill the CUs with 2-user
-// tiles (< 256 users): at U = 2,048 it measured 90.5 vs 85.9 ms per config-5 step (each slice's
+// tiles (< 256 two-user tiles, i.e. U <= 510): at U = 2,048 it measured 90.5 vs 85.9 ms per config-5 step (each slice's
 // top-k warms up on its own; its L2 hit rate is higher, 69 vs 45 %, but the stream is not what
 // bounds it). MINER_RK_SPLIT=1 / 0 forces either form.
-bool rk_split(const RkParams& prm) {
-  if (prm.ws_s == nullptr || prm.ws_i == nullptr || num_cus() != 256) return false;
+// Fewer than 256 two-user tiles means U <= 510.
+bool rk_split_wanted(int U) {
+  if (num_cus() != 256) return false;
   const char* ev = getenv("MINER_RK_SPLIT");
   if (ev && (ev[0] == '0' || ev[0] == '1')) return ev[0] == '1';
-  return (prm.U + kUT - 1) / kUT < num_cus();
+  return (U + kUT - 1) / kUT < num_cus();
+}
+bool rk_split(const RkParams& prm) {
+  if (prm.ws_s == nullptr || prm.ws_i == nullptr) return false;
+  return rk_split_wanted(prm.U);
 }
 
 template <class T, int NKT, int S, int GEO>
@@ -1045,6 +1050,7 @@ int miner_encode_users(void* stream, int dtype, const void* history, const int32
 
 size_t miner_rank_topk_workspace_bytes(int U, int topk) {
   if (U <= 0 || topk <= 0 || topk > kMaxTopk) return 0;
+  if (!rk_split_wanted(U)) return 0;     // the unsplit form needs no workspace
   return (size_t)U * kSplit * topk * 8;
 }
 

@@ -174,6 +174,42 @@ __device__ __forceinline__ void split8h(const float* x, u32x4& hi, u32x4& lo) {
   }
 }
 __device__ __forceinline__ uint2 lds_u64(const char* p) { return *reinterpret_cast<const uint2*>(p); }
+
+// e^x for the softmaxes' x = s - max <= 0: 2^(x·log2 e) on v_exp_f32 with the product's rounding
+// carried to first order (x·log2 e = yh + yl, yl from one fma and log2 e's low part; e^x =
+// 2^yh·(1 + yl·ln 2)), a few ulp like libm expf in 6 VALU instead of ~14 (its range reduction and
+// over/underflow selects); x is clamped at -104 (e^-104 underflows to 0 either way), so -inf gives 0
+__device__ __forceinline__ float x2_exp(float x) {
+  x = fmaxf(x, -104.0f);
+  const float yh = x * 1.4426950408889634f;
+  const float yl = __builtin_fmaf(x, 1.925963033500011e-8f, __builtin_fmaf(x, 1.4426950408889634f, -yh));
+  const float e = __builtin_amdgcn_exp2f(yh);
+  return __builtin_fmaf(e, yl * 0.69314718055994531f, e);
+}
+
+#ifndef X2_CAND_ASM
+#define X2_CAND_ASM 1
+#endif
+// wait for the LDS reads issued from asm into r / s (lgkmcnt(0)), the registers tied to the wait so
+// that no use moves above it
+template <int NT>
+__device__ __forceinline__ void x2_lds_wait(uint2 (&r)[NT][2], uint2 (&s)[NT][2]) {
+  if constexpr (NT == 1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]));
+  } else if constexpr (NT == 2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]),
+                 "+v"(r[1][0]), "+v"(r[1][1]), "+v"(s[1][0]), "+v"(s[1][1]));
+  } else if constexpr (NT == 3) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]),
+                 "+v"(r[1][0]), "+v"(r[1][1]), "+v"(s[1][0]), "+v"(s[1][1]),
+                 "+v"(r[2][0]), "+v"(r[2][1]), "+v"(s[2][0]), "+v"(s[2][1]));
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]),
+                 "+v"(r[1][0]), "+v"(r[1][1]), "+v"(s[1][0]), "+v"(s[1][1]),
+                 "+v"(r[2][0]), "+v"(r[2][1]), "+v"(s[2][0]), "+v"(s[2][1]),
+                 "+v"(r[3][0]), "+v"(r[3][1]), "+v"(s[3][0]), "+v"(s[3][1]));
+  }
+}
 __device__ __forceinline__ uint2 lds_tr(const char* p) {
   return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds_char*)p));
 }
@@ -505,7 +541,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     float sum = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      v[s] = expf(v[s] - mx);                // exp(-inf) = 0 past U (weight 0)
+      v[s] = x2_exp(v[s] - mx);              // 0 past U (v = -inf there; weight 0)
       sum = __builtin_fmaf(wm[s], v[s], sum);
     }
     sum = x_rows4_sum(sum);
@@ -613,14 +649,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (8 * kq + j < KK) {
-          const float pe = expf(lg[j] - mx);
+          const float pe = x2_exp(lg[j] - mx);
           sm += pe;
           num = __builtin_fmaf(pe, m[j], num);
         }
       }
       sm = x_rows4_sum(sm);
       num = x_rows4_sum(num);
-      sc = num / sm;
+      sc = num * __builtin_amdgcn_rcpf(sm);   // sm >= 1 (the max term): one rounding more than num / sm
     } else {
       if (p.score_type == MINER_SCORE_MAX) {
         float mx = -INFINITY;
@@ -692,8 +728,26 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
             make_float4(hx[ctl][0] * mui_scale, hx[ctl][1] * mui_scale, hx[ctl][2] * mui_scale, hx[ctl][3] * mui_scale);
     }
     if (mode & 2) {
-      const char* cpart = slot + 2 * kPart;
       uint2 cH_[NT][2], cL_[NT][2];
+#if X2_CAND_ASM
+      // plain ds_read_b64 from asm: hipcc pairs the q and q + 1 reads of one base into
+      // ds_read2st64_b64, whose 16-lane groups bank by dword mod 32, a 2-way conflict on these
+      // 16-row reads (MI355X_MICROARCH.md §LDS); ds_read_b64 banks mod 64 over 32 lanes: none.
+      // Their completion is waited for below (x2_lds_wait), before the candidate MFMAs.
+      {
+        const unsigned cb = lds_offset(slot);
+#pragma unroll
+        for (int ctl = 0; ctl < 2; ++ctl) {
+          const unsigned aH = cb + cfH[ctl], aL = cb + cfL[ctl];
+#pragma unroll
+          for (int q = 0; q < NT; ++q) {
+            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cH_[q][ctl]) : "v"(aH), "i"(2 * kPart + 4096 * q));
+            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cL_[q][ctl]) : "v"(aL), "i"(2 * kPart + 4096 * q));
+          }
+        }
+      }
+#else
+      const char* cpart = slot + 2 * kPart;
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
 #pragma unroll
@@ -702,6 +756,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           cL_[q][ctl] = lds_u64(cpart + cfL[ctl] + 4096 * q);
         }
       }
+#endif
       float x[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -715,6 +770,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
       u32x4 bH, bL;
       split8h(x, bH, bL);
+#if X2_CAND_ASM
+      x2_lds_wait<NT>(cH_, cL_);
+#endif
       X2_STAMP(5);
 #pragma unroll
       for (int q = 0; q < NT; ++q) {

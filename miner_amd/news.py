@@ -81,6 +81,12 @@ def x2_enabled() -> bool:
     return os.environ.get("MINER_NEWS_FP32", "x2") != "mfma32"
 
 
+def x2_fits(n_news: int, d: int) -> bool:
+    """The pair planes of an [n_news, d] table fit the x2 kernel's 32-bit row offsets
+    (miner_score_news_x2 returns MINER_ESHAPE past n_news·d·4 = 2^32 - 1, e.g. > 1.39M news at d = 768)."""
+    return n_news * d * 4 <= 0xFFFFFFFF
+
+
 def split_x2(src: Tensor, out: Optional[Tensor] = None, ws: Optional[Tensor] = None):
     """fp32 [n, d] -> (pairs [n, 2d] fp16, workspace with the scale) (miner_news_split_x2)."""
     _require_device(src)
@@ -131,7 +137,15 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
                                               pw.Dc, pw.K, _ptr(logits), _ptr(proj))
     _lib.check(rc, "miner_news_precompute")
     planes = None
-    if dtype == torch.float32 and (x2_enabled() if x2 is None else x2):
+    want_x2 = dtype == torch.float32 and (x2_enabled() if x2 is None else x2)
+    if want_x2 and not x2_fits(n_news, d):
+        # the pair-plane kernel addresses a row piece with a 32-bit byte offset (news_x2.hip,
+        # MINER_ESHAPE past it): such a table scores on the fp32-MFMA kernel instead
+        if x2:
+            raise ValueError(f"x2=True: a {n_news} x {d} table is past the pair-plane kernel's 4 GiB "
+                             "row-offset range (n_news * d * 4 < 2^32)")
+        want_x2 = False
+    if want_x2:
         o = out.x2 if out is not None and out.x2 is not None else None
         t2, tws = split_x2(table, None if o is None else o.table2, None if o is None else o.table_ws)
         p2, pws = (split_x2(proj, None if o is None else o.proj2, None if o is None else o.proj_ws)

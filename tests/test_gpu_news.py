@@ -164,6 +164,59 @@ def test_x2_error_vs_fp32_mfma(scale, score_type, monkeypatch):
     assert errs["x2"][1] <= 1.5 * errs["mfma32"][1] + 1e-8 * rms, errs
 
 
+def _heavy_tailed(seed, B=240, L=50, d=768, n_news=4000, C=40):
+    """A news table with the outliers encoder outputs have: three dimensions 100x the rest in every
+    row, row 1 at 1e4x and row 2 at 1e5x the median row norm; impressions 0-79 touch the outlier
+    rows (in the history: 0-19 row 1, 20-39 row 2; as a candidate: 40-59 row 1, 60-79 row 2),
+    the rest never do."""
+    g = torch.Generator().manual_seed(seed)
+    t = torch.randn((n_news, d), generator=g) / d ** 0.5
+    t[:, [5, 77, 400]] *= 100.0
+    t[1] *= 1e4
+    t[2] *= 1e5
+    hid = torch.randint(3, n_news, (B, L), generator=g)
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    mask = torch.arange(L)[None, :] >= (L - lens)[:, None]
+    hid[~mask] = 0
+    cid = torch.randint(3, n_news, (B, C), generator=g)
+    hid[0:20, L - 1] = 1
+    hid[20:40, L - 1] = 2
+    cid[40:60, 7] = 1
+    cid[60:80, 3] = 2
+    W1, Q, W2 = synthetic.init_weights(seed, d, 200, 32, device=DEV)
+    return t.to(DEV), hid.to(DEV), mask.to(DEV), cid.to(DEV), W1, Q, W2
+
+
+@pytest.mark.parametrize("score_type", ["max", "weighted"])
+def test_x2_heavy_tailed(score_type, monkeypatch):
+    """Heavy-tailed tables (rows 1e4x and 1e5x the median norm, a few dimensions 100x the rest):
+    the fp16-pair kernel against float64 on the impressions that never touch the outlier rows, with
+    the fp32 bar's rms taken over those impressions alone (an outlier row must not hide the error of
+    the ordinary rows behind its own magnitude), and within 1.5x the fp32-MFMA kernel's error there;
+    on the impressions that touch the outliers too for 'max' (for 'weighted' the softmax over K of
+    such an impression is one-hot and ill-conditioned in any fp32 form: error ratio only)."""
+    table, hid, mask, cid, W1, Q, W2 = _heavy_tailed(35)
+    ref = _f64_scores(table, hid, mask, cid, W1, Q, W2, score_type)
+    subsets = {"ordinary": slice(80, None), "outlier": slice(0, 80)}
+    errs = {}
+    for kern in FP32_KERNELS:
+        monkeypatch.setenv("MINER_NEWS_FP32", kern)
+        nt = news.precompute(table, W1, Q, W2)
+        s = news.score(nt, hid, mask, cid, score_type=score_type).double().cpu()
+        torch.cuda.synchronize()
+        for name, sl in subsets.items():
+            r, x = ref[sl], s[sl]
+            rms = float(r.pow(2).mean().sqrt())
+            e = (x - r).abs()
+            errs[(kern, name)] = (float((e / (r.abs() + rms)).max()), float(e.pow(2).mean().sqrt() / rms))
+            if name == "ordinary" or score_type == "max":
+                _ok(x, r, torch.float32, f"{kern} {score_type} on the {name} impressions")
+    for name in subsets:
+        xe, me = errs[("x2", name)], errs[("mfma32", name)]
+        assert xe[0] <= 1.5 * me[0] + 1e-7, (name, errs)
+        assert xe[1] <= 1.5 * me[1] + 1e-8, (name, errs)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("d,Dc,K", [(64, 32, 4), (256, 200, 32), (768, 200, 32), (192, 72, 16)])
 def test_precompute_vs_f64(dtype, d, Dc, K):
@@ -308,19 +361,26 @@ def test_bad_inputs_raise():
         news.precompute(table[:, :96].contiguous(), W1[:, :96].contiguous(), Q, None, with_proj=False)
 
 
+@pytest.mark.parametrize("shp_rt", [True, False])
 @pytest.mark.parametrize("B,L,d,C,K,ragged", [
-    (300, 50, 768, 40, 32, None),      # config 3 shape
-    (700, 50, 256, 40, 32, None),      # config 2 shape (compile-time d = 256 form)
+    (300, 50, 768, 40, 32, None),      # config 3 shape (compile-time MIND-shape LOSS kernel unless shp_rt)
+    (700, 50, 256, 40, 32, None),      # config 2 shape (compile-time d = 256 LOSS kernel unless shp_rt)
     (257, 20, 64, 5, 4, None),         # config 1 shape: one chunk per row, K = 4
     (90, 64, 128, 33, 16, None),       # L = 64, K = 16 (interest tile 1 empty)
     (40, 37, 320, 150, 12, None),      # three candidate passes
-    (211, 50, 768, None, 32, (0, 150)),  # ragged 0..150 candidates
+    (211, 50, 768, None, 32, (0, 150)),  # ragged 0..150 candidates (compile-time LOSS kernel unless shp_rt)
 ])
-def test_fused_disagreement(B, L, d, C, K, ragged, monkeypatch):
+def test_fused_disagreement(B, L, d, C, K, ragged, shp_rt, monkeypatch):
     """The eval loss's disagreement term formed inside the fp32 scoring kernel (the Gram matrix of
     mui, no mui written) equals the reference formula on the reference's own mui (float64), and the
-    scores of the loss variant match the plain kernel's (its run-time-shape form) at the fp32 bar."""
-    monkeypatch.setenv("MINER_NEWS_SHP_RT", "1")
+    scores of the loss variant match the plain kernel's at the fp32 bar. With shp_rt unset the MIND
+    shape (L = 50, K = 32, no bias, no mui output) runs the compile-time LOSS kernels
+    (news_score_x2<WEIGHTED, *, 12 | 4, 2, true>) that eval_loop's fused-loss path launches by
+    default; their D and scores must also match the run-time-shape form's."""
+    if shp_rt:
+        monkeypatch.setenv("MINER_NEWS_SHP_RT", "1")
+    else:
+        monkeypatch.delenv("MINER_NEWS_SHP_RT", raising=False)
     from miner_amd import evaluation
     table, hid, mask, cid, offs, W1, Q, W2 = _setup(B + d + K, B, L, d, 2000, torch.float32, C=C or 40, K=K,
                                                     ragged=ragged)
@@ -330,9 +390,18 @@ def test_fused_disagreement(B, L, d, C, K, ragged, monkeypatch):
     torch.cuda.synchronize()
     # same arithmetic; hipcc may contract a multiply-add differently in the two instantiations
     _ok(s, s_plain, torch.float32, "loss-variant scores vs the plain kernel")
-    ref_mui, _ = _oracle(table, hid, mask, cid, offs, W1, Q, W2)
+    ref_mui, ref_s = _oracle(table, hid, mask, cid, offs, W1, Q, W2)
+    _ok(s, ref_s, torch.float32, "loss-variant scores vs the oracle")
     ref = evaluation.disagreement(ref_mui.double()).float()
     _ok(dis, ref, torch.float32, "disagreement")
+    if not shp_rt:
+        # the compile-time-shape kernels against the run-time form on the same inputs
+        monkeypatch.setenv("MINER_NEWS_SHP_RT", "1")
+        s_rt, dis_rt = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True, disagreement=True)
+        torch.cuda.synchronize()
+        monkeypatch.delenv("MINER_NEWS_SHP_RT")
+        _ok(s, s_rt, torch.float32, "compile-time-shape LOSS scores vs the run-time form")
+        _ok(dis, dis_rt, torch.float32, "compile-time-shape disagreement vs the run-time form")
     # mui-only launch with the loss epilogue (score type 'none')
     m2, d2 = news.score(nt, hid, mask, score_type="none", x2=True, disagreement=True)
     torch.cuda.synchronize()

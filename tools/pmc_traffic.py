@@ -22,6 +22,8 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from tools.srcsha import KERNEL_SOURCES, source_sha16  # noqa: E402
 KERNEL_TAG = "miner_fusedIDF16bLi0E"     # mangled miner_fused<__bf16, kFull, ...>
 KERNEL_TAGS = [KERNEL_TAG, "miner_fused<__bf16, 0"]
 
@@ -38,11 +40,15 @@ def read_counters(d):
                 did = row.get("Dispatch_Id") or row.get("Correlation_Id")
                 per[did][row["Counter_Name"]] += float(row["Counter_Value"])
                 names[did] = kn
+                SYMBOLS.add(kn)
     out = defaultdict(list)
     for did, cs in per.items():
         for c, v in cs.items():
             out[c].append(v)
     return {c: statistics.median(v) for c, v in out.items()}, len(per)
+
+
+SYMBOLS = set()     # the kernel names the counter rows matched
 
 
 def main():
@@ -60,6 +66,8 @@ def main():
                     help="kernel-name substrings to match (mangled and demangled), with --workload / --kernel-name")
     ap.add_argument("--workload", default=None)
     ap.add_argument("--kernel-name", default=None)
+    ap.add_argument("--source", default=None, choices=sorted(KERNEL_SOURCES),
+                    help="kernel family whose sources the passes measured (bench.py rejects the file once they change)")
     args = ap.parse_args()
     workload, kernel = "L50_K32_d768_Dc200_C40_bf16", "miner_fused<bf16,full>"
     if args.tag:
@@ -92,7 +100,13 @@ def main():
         "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,
         "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count of 16B/lane streams), KiB -> bytes",
+        "kernel_symbols": sorted(SYMBOLS),
     }
+    src = args.source or ("news_x2" if args.tag and any("news_score_x2" in t for t in args.tag) else
+                          "news" if (args.news or args.news32 or (args.tag and any("news_score" in t for t in args.tag)))
+                          else "miner_score")
+    res["source_files"] = list(KERNEL_SOURCES[src])
+    res["source_sha16"] = source_sha16(KERNEL_SOURCES[src])
     if "SQ_VALU_MFMA_BUSY_CYCLES" in med and "GRBM_GUI_ACTIVE" in med:
         res["SQ_VALU_MFMA_BUSY_CYCLES"] = med["SQ_VALU_MFMA_BUSY_CYCLES"]
         res["GRBM_GUI_ACTIVE"] = med["GRBM_GUI_ACTIVE"]

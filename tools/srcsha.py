@@ -1,0 +1,23 @@
+"""The source identity a PMC counter file is bound to (tools/pmc_traffic.py writes it, bench.py checks
+it): sha256 over the repo-relative path and bytes of each kernel source a counter pass measured, so a
+kernel edited after its profiling pass cannot carry stale counters into a bench line."""
+import hashlib
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# the sources each profiled kernel family is compiled from
+KERNEL_SOURCES = {
+    "news_x2": ("miner_amd/csrc/news_x2.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_news.h"),
+    "news": ("miner_amd/csrc/news.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_news.h"),
+    "miner_score": ("miner_amd/csrc/miner_score.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_score.h"),
+}
+
+
+def source_sha16(files) -> str:
+    h = hashlib.sha256()
+    for rel in files:
+        h.update(rel.encode())
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
