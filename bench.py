@@ -243,9 +243,10 @@ NEWS_B = 3_000_000   # impressions per GPU per step: the whole MIND-large-shaped
 C2_B, C2_D, C2_NEWS = 50_000, 256, 65_238   # config 2 (MIND-small shape: ~65k news)
 
 
-def news_batch(seed, B, n_news, dev, chunk=1 << 20):
+def news_batch(seed, B, n_news, dev, chunk=1 << 20, full=False):
     """Impressions as news ids (the reference's eval input, reader.py:351-379): history length
-    ~ U{0..L}, left-padded with the pad news (row 0, reader.py:101-110, :369); candidates uniform."""
+    ~ U{0..L}, left-padded with the pad news (row 0, reader.py:101-110, :369); candidates uniform.
+    ``full``: every history holds L clicks (no padding: the most rows gathered per impression)."""
     g = torch.Generator(device=dev).manual_seed(seed)
     hid = torch.empty((B, L), dtype=torch.int32, device=dev)
     mask = torch.empty((B, L), dtype=torch.bool, device=dev)
@@ -253,7 +254,7 @@ def news_batch(seed, B, n_news, dev, chunk=1 << 20):
     pos = torch.arange(L, device=dev)
     for s in range(0, B, chunk):
         e = min(s + chunk, B)
-        lens = torch.randint(0, L + 1, (e - s,), generator=g, device=dev)
+        lens = torch.full((e - s,), L, device=dev) if full else torch.randint(0, L + 1, (e - s,), generator=g, device=dev)
         m = pos[None, :] >= (L - lens)[:, None]
         h = torch.randint(1, n_news, (e - s, L), generator=g, device=dev, dtype=torch.int32)
         hid[s:e] = torch.where(m, h, torch.zeros_like(h))
@@ -551,6 +552,23 @@ def run_news(args, rank, world, dev):
                      "unit": "pairs/s", "ms_per_launch": round(ms_l, 4), "impressions": B,
                      "vs_plain_kernel": round(kern32 / ms_l, 4)}
         del res
+    # every history full (hist_len = L, no left padding): the masked-slot grouping saves nothing here
+    full_hist = None
+    if world == 1 and not args.no_exact:
+        pool_f = [news_batch(4000, B, N_NEWS, dev, full=True)]
+        n_f = min(args.steps, 5)
+        elf, _, kernf, _, _ = measure_news(table32, W1, Q, W2, pool_f, n_f, 1, world, dev, x2=True)
+        rf = roofline_news(B, kernf, 4, mode="x2",
+                           pmc=load_pmc(args.news_traffic32_full, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_fp32_full", B,
+                                        "news_x2"),
+                           kernel="news_score_x2<weighted, dense, 12 chunks, MIND shape>, full histories")
+        gathered = news_gathered_bytes(L, D, C, K, 4)
+        full_hist = {"histories": f"all {L} slots clicked (no padding)", "steps": n_f,
+                     "value": round(B * C * n_f / elf, 1), "unit": "pairs/s", "ms_per_step": round(elf / n_f * 1e3, 4),
+                     "kernel_ms": round(kernf, 4), "roofline": rf,
+                     "gathered_over_algorithmic_bytes": round(gathered / bytes_per_impression(L, D, C, 4), 4),
+                     "vs_headline_kernel_ms": round(kernf / kern32, 4)}
+        del pool_f
     # bf16 throughput mode, same batch and protocol
     table16 = table32.to(torch.bfloat16)
     el16, pre16, kern16, o16, nt16 = measure_news(table16, W1, Q, W2, pool, args.steps, args.warmup, world, dev)
@@ -623,7 +641,7 @@ def run_news(args, rank, world, dev):
         "precompute": {"kernels": "news_pre<fp32> + x2_absmax/x2_split of the table and of proj", "ms": round(pre32, 4),
                        "flops": pre_fl, "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
                        "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
-        "fp32_mfma_exact": exact, "eval_with_loss": loss_line, "weak_scaling": weak,
+        "fp32_mfma_exact": exact, "eval_with_loss": loss_line, "full_histories": full_hist, "weak_scaling": weak,
         "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "metric_step": metric_step,
         "dense_rows_kernel": dense, "with_host_tolist": with_host,
         "cpu_baseline": cpu, "auc_parity": auc, "pmc_status": PMC_STATUS,
@@ -1088,6 +1106,7 @@ def main():
     ap.add_argument("--news-traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_news.json"))
     ap.add_argument("--news-traffic32", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_x2.json"))
     ap.add_argument("--news-traffic32x", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_fp32.json"))
+    ap.add_argument("--news-traffic32-full", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_x2_full.json"))
     ap.add_argument("--news-traffic-c2", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_c2.json"))
     ap.add_argument("--news-traffic-c2-32", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_c2_x2.json"))
     ap.add_argument("--no-exact", action="store_true", help="skip the fp32-MFMA (news_score32) sub-line")

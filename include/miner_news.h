@@ -81,20 +81,20 @@ int miner_score_news(void* stream, int dtype, int score_type, const void* news_t
  * fp32; fp32 accumulation). The pair table takes 4 bytes per element, as fp32.
  *
  * miner_news_split_x2: src [n, d] fp32 -> dst [n, d] pairs: per row, per 64-column chunk, the 64
- *   hi then the 64 lo fp16 values (256 bytes); workspace: miner_news_x2_workspace_floats() floats,
- *   workspace[0] = s, workspace[1] = 1/s on return (the scale handle miner_score_news_x2 takes).
+ *   hi then the 64 lo fp16 values (256 bytes) of x / u_r, with one power-of-two unit per row
+ *   u_r = 2^(e_r - 14), max|row r| < 2^e_r, written to row_unit[r] (n floats, device memory).
  *   Apply it to the news table (the x2 table) and to miner_news_precompute's fp32 news_proj.
- * miner_score_news_x2: miner_score_news (fp32) from the pair tables: table_scale / proj_scale are
- *   the workspaces of the two splits (proj2 / proj_scale NULL unless score_type == WEIGHTED).
+ *   d % 64 == 0, d <= 1024.
+ * miner_score_news_x2: miner_score_news (fp32) from the pair tables: table_unit / proj_unit are
+ *   the row units of the two splits (proj2 / proj_unit NULL unless score_type == WEIGHTED).
  *   Same limits, plus n_news·d·4 < 2^32 (32-bit row offsets). disagree_out [B] fp32 or NULL:
  *   the eval loss's per-impression disagreement term, mean over k != k' of cos(mui_k, mui_k') with
  *   the diagonal zeroed (src/loss.py:81, src/utils.py:9-29), formed in the kernel from the Gram
  *   matrix of mui (no mui is written unless user_out is given).
  */
-size_t miner_news_x2_workspace_floats(void);
-int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* workspace);
-int miner_score_news_x2(void* stream, int score_type, const void* table2, const float* table_scale,
-                        const float* news_logits, const void* proj2, const float* proj_scale,
+int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* row_unit);
+int miner_score_news_x2(void* stream, int score_type, const void* table2, const float* table_unit,
+                        const float* news_logits, const void* proj2, const float* proj_unit,
                         int n_news, const int32_t* his_ids, const uint8_t* his_mask,
                         const float* his_bias, const int32_t* cand_ids, const int32_t* cand_offsets,
                         int B, int L, int C, int d, int K, float* scores, float* user_out,

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MINER_HIP_LIB", os.path.join(_HERE, "libminer_hip.so"
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
 SCORE_WEIGHTED, SCORE_MAX, SCORE_MEAN, SCORE_NONE = 0, 1, 2, 3
 SCORE_TYPES = {"weighted": SCORE_WEIGHTED, "max": SCORE_MAX, "mean": SCORE_MEAN, "none": SCORE_NONE}
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every symbol include/*.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
@@ -50,7 +50,6 @@ SIGNATURES = {
     "miner_news_precompute": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _P]),
     "miner_score_news": (_I, [_P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "miner_news_supported": (_I, [_I, _I, _I, _I, _I]),
-    "miner_news_x2_workspace_floats": (ctypes.c_size_t, []),
     "miner_news_split_x2": (_I, [_P, _P, _I, _I, _P, _P]),
     "miner_score_news_x2": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     # include/miner_wide.h

@@ -4,8 +4,10 @@
 // Why. The fp32 scoring kernel news_score32 (news.hip) runs its contractions on the fp32 MFMA:
 // 64 FLOP/clk/SIMD, and it excludes the VALU of its SIMD, so the GELU and every other vector
 // instruction add to the MFMA time (round-2 verdict: MFMA-bound at 0.56 of the fp32 peak). Here
-// every fp32 operand x is carried as an exact-sum pair of fp16 values in a power-of-two scale s,
-//     x·s = hi + lo,  hi = fp16(x·s),  lo = fp16(x·s − hi)          (|x·s − hi − lo| ≤ 2⁻²²·|x·s|)
+// every fp32 operand x is carried as an exact-sum pair of fp16 values in a power-of-two scale s
+// (per table row, or per interest for the attention weights and the user vectors),
+//     x·s = hi + lo,  hi = fp16(x·s),  lo = fp16(x·s − hi)          (|x·s − hi − lo| ≤ 2⁻²²·|x·s|
+//                                                                    while lo is a normal fp16)
 // and a product a·b is the three partial products lo_a·hi_b + hi_a·lo_b + hi_a·hi_b on
 // v_mfma_f32_16x16x32_f16 (every fp16 x fp16 product is exact in fp32, the accumulation is fp32;
 // the dropped lo_a·lo_b is below 2⁻²²·|a·b|). The operand error is the fp32 rounding's order, far
@@ -16,9 +18,12 @@
 // the same as fp32, so the gathered bytes do not grow.
 //
 // Kernels:
-//   x2_absmax    per-block max |x| of an fp32 table (partials for the scale)
-//   x2_split     the scale s = 2^(14 − ⌈log2 max|x|⌉) (so |x·s| ≤ 2^14 < 65504) and the pair planes:
-//                row n, 64-column chunk cc: [hi of the 64 columns | lo of the 64 columns], 256 B
+//   x2_split_rows  the pair planes with one power-of-two unit per ROW: row n holds x / u_n with
+//                u_n = 2^(e_n - 14), max|row n| < 2^e_n (so every |x / u_n| < 2^14 < 65504); per
+//                64-column chunk cc: [hi of the 64 columns | lo of the 64 columns], 256 B. A
+//                per-row unit keeps each row's lo plane out of the fp16 subnormals however far its
+//                magnitude is from the table's largest row (tests/test_gpu_news.py heavy-tailed
+//                tables: rows 1e4x and 1e5x the median norm)
 //   news_score_x2  per impression (one persistent workgroup of 8 waves per CU), from the ids:
 //                A   = softmax_L(logits[his] + bias, masked slots = 1e-30)  (model.py:176-181)
 //                mui = A·E[his]                                             (model.py:182)
@@ -52,6 +57,10 @@
 
 namespace {
 
+#ifndef X2_DMA_SPLIT
+#define X2_DMA_SPLIT 0
+#endif
+constexpr int kNB = X2_DMA_SPLIT ? 4 : 2;              // row-DMA blocks per wave per part
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kMaxL = 64;
@@ -110,7 +119,7 @@ __device__ __forceinline__ void x2_dma_row(uint32_t off, const char* base, unsig
   unsigned t;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
                "s_mov_b32 m0, %0"
-               : "=&s"(t) : "v"(off), "s"(base), "s"(m) : "memory");
+               : "=&s"(t) : "v"(off), "s"(base), "s"(__builtin_amdgcn_readfirstlane(m)) : "memory");
 }
 __device__ __forceinline__ void x2_dma_b128(const void* g, unsigned lds) {
   unsigned t;
@@ -147,13 +156,13 @@ __device__ __forceinline__ void split2(float x0, float x1, unsigned& hi, unsigne
   hi = hb;
   lo = __builtin_bit_cast(unsigned, l);
 }
-// the attention weights w·e·c (w a small integer multiplicity, e = exp, c = kSA / Σ) -> (hi, lo)
+// the attention weights w·e·c (w a small integer multiplicity, e = exp, c = κ·unit / Σ) -> (hi, lo)
 // fp16 pairs with the residual taken from exact products (fma), so a group of m slots carries one
 // rounding of its weight, not the three of w·(e·c) rounded step by step
-__device__ __forceinline__ void split2w(float w0, float e0, float w1, float e1, float c, unsigned& hi,
+__device__ __forceinline__ void split2w(float w0, float e0, float c0, float w1, float e1, float c1, unsigned& hi,
                                         unsigned& lo) {
-  const float p0 = e0 * c, p1 = e1 * c;
-  const float q0 = __builtin_fmaf(e0, c, -p0), q1 = __builtin_fmaf(e1, c, -p1);
+  const float p0 = e0 * c0, p1 = e1 * c1;
+  const float q0 = __builtin_fmaf(e0, c0, -p0), q1 = __builtin_fmaf(e1, c1, -p1);
   const f16x2 h = {(_Float16)(w0 * p0), (_Float16)(w1 * p1)};
   unsigned hb = __builtin_bit_cast(unsigned, h);
   asm volatile("" : "+v"(hb));
@@ -187,9 +196,26 @@ __device__ __forceinline__ float x2_exp(float x) {
   return __builtin_fmaf(e, yl * 0.69314718055994531f, e);
 }
 
-#ifndef X2_CAND_ASM
-#define X2_CAND_ASM 1
-#endif
+// the transposed history operand pieces of 32-row block KB (8 ds_read_b64_tr_b16 from asm): lane
+// offsets trH / trL (hi / lo plane) from the history part's LDS address hb
+template <int KB>
+__device__ __forceinline__ void x2_tr_reads(unsigned hb, const uint32_t (&trH)[2][2], const uint32_t (&trL)[2][2],
+                                            uint2 (&rh)[2][2], uint2 (&rl)[2][2]) {
+#pragma unroll
+  for (int ctl = 0; ctl < 2; ++ctl) {
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(rh[ctl][rr]) : "v"(hb + trH[ctl][rr]), "i"(8192 * KB));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(rl[ctl][rr]) : "v"(hb + trL[ctl][rr]), "i"(8192 * KB));
+    }
+  }
+}
+// wait until at most N LDS operations are in flight, the 8 history pieces tied to the wait
+template <int N>
+__device__ __forceinline__ void x2_tr_wait(uint2 (&rh)[2][2], uint2 (&rl)[2][2]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)" : "+v"(rh[0][0]), "+v"(rh[0][1]), "+v"(rh[1][0]), "+v"(rh[1][1]),
+               "+v"(rl[0][0]), "+v"(rl[0][1]), "+v"(rl[1][0]), "+v"(rl[1][1]) : "i"(N));
+}
 // wait for the LDS reads issued from asm into r / s (lgkmcnt(0)), the registers tied to the wait so
 // that no use moves above it
 template <int NT>
@@ -217,59 +243,58 @@ __device__ __forceinline__ uint2 lds_tr(const char* p) {
 // ================================================================================================
 // pair planes
 // ================================================================================================
-constexpr int kAbsBlocks = 256;
-
-__global__ __launch_bounds__(256) void x2_absmax(const float* __restrict__ src, size_t n, float* __restrict__ part) {
-  __shared__ float red[4];
-  float m = 0.f;
-  const size_t n4 = n >> 2;
-  const float4* s4 = reinterpret_cast<const float4*>(src);
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-    const float4 v = s4[i];
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-  }
-  for (size_t i = (n4 << 2) + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) m = fmaxf(m, fabsf(src[i]));
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-}
-
-// the scale from the partials: a power of two with max|x|·s <= 2^14 (1 for an all-zero or
-// non-finite table; an infinite or NaN entry then stays one in its pair)
-__device__ __forceinline__ float x2_scale(const float* part, int np) {
-  float m = 0.f;
-  for (int i = 0; i < np; ++i) m = fmaxf(m, part[i]);
-  if (!(m > 0.f) || !isfinite(m)) return 1.0f;
+// the unit of a row from its max |x|: u = 2^(e - 14) with max|x| < 2^e, so the pair values x / u
+// stay below 2^14 (< 65504); e clamped to [-110, 128] (1 / u representable); an all-zero row gets
+// u = 2^-14, a non-finite max u = 1 (an infinite or NaN entry then stays one in its pair)
+__device__ __forceinline__ int x2_row_exp(float m) {
+  if (!(m > 0.f)) return 0;
+  if (!isfinite(m)) return 14;
   int e;
   frexpf(m, &e);                                     // m = f·2^e, f in [0.5, 1)
-  return ldexpf(1.0f, min(max(14 - e, -126), 127));
+  return min(max(e, -110), 128);
 }
 
-// dst row n: for each 64-column chunk, 64 hi then 64 lo fp16 (the x2 layout); scale_out = {s, 1/s}
-__global__ __launch_bounds__(256) void x2_split(const float* __restrict__ src, int N, int d, const float* __restrict__ part,
-                                                unsigned short* __restrict__ dst, float* __restrict__ scale_out) {
-  __shared__ float sc;
-  if (threadIdx.x == 0) sc = x2_scale(part, kAbsBlocks);
-  __syncthreads();
-  const float s = sc;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    scale_out[0] = s;
-    scale_out[1] = 1.0f / s;
-  }
+// one wave per row: dst row n = for each 64-column chunk, 64 hi then 64 lo fp16 of x / u_n (the x2
+// layout); unit[n] = u_n. A per-row unit (not one per table) keeps every row's lo plane out of the
+// fp16 subnormals when one row of the table is many orders of magnitude larger than the others
+constexpr int kSplitMaxG = 2;                         // 8-column groups per lane: d <= 1024
+__global__ __launch_bounds__(256) void x2_split_rows(const float* __restrict__ src, int N, int d,
+                                                     unsigned short* __restrict__ dst, float* __restrict__ unit) {
+  const int lane = threadIdx.x & 63;
   const int g8 = d >> 3;                             // groups of 8 columns per row
-  const size_t total = (size_t)N * g8;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-    const size_t n = i / g8;
-    const int c0 = (int)(i - n * g8) * 8;
-    const float4* p = reinterpret_cast<const float4*>(src + n * d + c0);
-    const float4 a = p[0], b = p[1];
-    const float x[8] = {a.x * s, a.y * s, a.z * s, a.w * s, b.x * s, b.y * s, b.z * s, b.w * s};
-    u32x4 hi, lo;
-    split8h(x, hi, lo);
-    unsigned short* row = dst + n * (size_t)(2 * d) + (c0 >> 6) * 128 + (c0 & 63);
-    *reinterpret_cast<u32x4*>(row) = hi;
-    *reinterpret_cast<u32x4*>(row + 64) = lo;
+  for (int n = blockIdx.x * 4 + (threadIdx.x >> 6); n < N; n += gridDim.x * 4) {
+    const float* row = src + (size_t)n * d;
+    float4 v[kSplitMaxG][2];
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < kSplitMaxG; ++j) {
+      const int gi = lane + 64 * j;
+      if (gi < g8) {
+        const float4* q = reinterpret_cast<const float4*>(row + 8 * gi);
+        v[j][0] = q[0];
+        v[j][1] = q[1];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[j][0].x), fabsf(v[j][0].y)), fmaxf(fabsf(v[j][0].z), fabsf(v[j][0].w))));
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[j][1].x), fabsf(v[j][1].y)), fmaxf(fabsf(v[j][1].z), fabsf(v[j][1].w))));
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const int e = x2_row_exp(m);
+    const float s = ldexpf(1.0f, 14 - e);
+    if (lane == 0) unit[n] = ldexpf(1.0f, e - 14);
+#pragma unroll
+    for (int j = 0; j < kSplitMaxG; ++j) {
+      const int gi = lane + 64 * j;
+      if (gi < g8) {
+        const float x[8] = {v[j][0].x * s, v[j][0].y * s, v[j][0].z * s, v[j][0].w * s,
+                            v[j][1].x * s, v[j][1].y * s, v[j][1].z * s, v[j][1].w * s};
+        u32x4 hi, lo;
+        split8h(x, hi, lo);
+        const int c0 = 8 * gi;
+        unsigned short* o = dst + (size_t)n * (2 * d) + (c0 >> 6) * 128 + (c0 & 63);
+        *reinterpret_cast<u32x4*>(o) = hi;
+        *reinterpret_cast<u32x4*>(o + 64) = lo;
+      }
+    }
   }
 }
 
@@ -291,11 +316,11 @@ __device__ unsigned long long g_x2_items;
 #endif
 
 struct X2Params {
-  const void* table2;      // [n_news, d] pairs (x2 layout), scale sc_t
+  const void* table2;      // [n_news, d] pairs (x2 layout): row n holds x / unit_t[n]
   const float* logits;     // [n_news, K]
-  const void* proj2;       // [n_news, d] pairs, scale sc_p (weighted only)
-  const float* sc_t;       // {s, 1/s}
-  const float* sc_p;
+  const void* proj2;       // [n_news, d] pairs, row n = x / unit_p[n] (weighted only)
+  const float* unit_t;     // [n_news] per-row units (powers of two, x2_split_rows)
+  const float* unit_p;
   const int32_t* his_ids;
   const uint8_t* mask;
   const float* bias;
@@ -345,12 +370,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   const char* tabB = static_cast<const char*>(p.table2);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj2) : tabB;
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
-  // scales: the history product accumulates s_A·s_part·(A·part)
-  const float iE = p.sc_t[1];
-  const float sPj = WEIGHTED ? p.sc_p[0] : 1.0f, iPj = WEIGHTED ? p.sc_p[1] : 1.0f;
-  const float op_scale = P == 0 ? 1.0f / kSA : (1.0f / kSA) * iPj;   // acc -> s_E·mui | x
-  const float mui_scale = (1.0f / kSA) * iE;                          // acc -> mui
-  const float m_scale = iE * iE, lg_scale = iE * iPj;                 // S7: M_s, Lg_s -> M, Lg
+  // Scales. Pair-plane row u holds part_u / unit_u; the history product's B operand is
+  // κ_k·A_ku·unit_u (κ_k a power of two per interest, softmax_inwave), so it accumulates
+  // acc_k = κ_k·(A·part)_k. Per lane (its interest k): the accumulator -> split operand factor
+  // (mui path 2^-14: |κ_k·mui_k| < 2^28; X path 1/κ_k, the GELU's input), the X path's factor after
+  // the GELU (κ_k·2^-14), the pass-end factor of the M / Lg partials (2^14 / κ_k, leaving only the
+  // candidate's unit for S7) and 1 / κ_k for the mui output. Set per impression.
+  float kap = kSA;                         // κ_k of this lane's interest (the wave's path), per impression
+  float uc_pend = 1.0f;                    // S7 lane's candidate unit (X waves), loaded a chunk ahead
 
   auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
   auto cands = [&](int i, int& off, int& cnt) {
@@ -416,6 +443,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     int* his = l1_his(smem, i & 3);
     const int ls = min(l, L - 1);
     const int id = his[ls];
+    // the rows' units (biased exponents eb = e + 127 of unit = 2^(e - 14)), loaded now, used below
+    const int idc = min(max(id, 0), p.n_news - 1);
+    const float uE = p.unit_t[idc];
+    const float uP = WEIGHTED ? p.unit_p[idc] : 1.0f;
     const uint32_t mw = l1_mask(smem, i & 3)[ls];
     const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + ls) & 3);
     const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
@@ -432,22 +463,31 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int U = __popcll(bal);
     const int uidx = __popcll(bal & ((1ull << l) - 1ull));
     float* pr = prep_blk(smem, i);
-    if (uniq) {                          // (±m, add): the sign says click / pad, |.| the multiplicity
+    // (±code, add): the sign says click / pad; |code| = m + 128·ebE + 32768·ebP (< 2^24, exact):
+    // the multiplicity and the two rows' unit exponents
+    const int ebE = ((__float_as_int(uE) >> 23) & 255) + 14, ebP = ((__float_as_int(uP) >> 23) & 255) + 14;
+    if (uniq) {
       his[uidx] = id;
-      pr[uidx] = keep ? (float)m : -(float)m;
+      const float code = (float)(m + 128 * ebE + 32768 * ebP);
+      pr[uidx] = keep ? code : -code;
       pr[64 + uidx] = keep ? bv : 1e-30f;
     }
-    if (l >= U) {                        // every coefficient past the groups (a unique lane may sit there)
-      pr[l] = 0.f;
+    if (l >= U) {                        // every coefficient past the groups (a unique lane may sit there):
+      pr[l] = (float)(128 * 127 + 32768 * 127);   // m = 0, units 2^-14
       pr[64 + l] = -INFINITY;
     }
     if (l == 0) dup_u(smem, i & 3)[0] = U;
   };
-  // row DMAs of a chunk: wave w issues the 4-row blocks w and 8 + (w ^ 4) of every part (the rows
-  // 32..47, live for L = 50 / C = 40, go to the X waves, the mostly-padding rows 48..63 to the mui
-  // waves). Lane l fills row 4b + (l >> 4), chunk slot l & 15 from source chunk slot ^ x2swz(row).
-  // lv bit jj: history rows of block jj live; bit 2 + jj: its candidate rows live.
-  auto dma_block = [&](int jj) { return jj ? 8 + (wave ^ 4) : wave; };
+  // row DMAs of a chunk. X2_DMA_SPLIT 0: wave w issues the 4-row blocks w and 8 + (w ^ 4) of every
+  // part (the rows 32..47, live for L = 50 / C = 40, go to the X waves, the mostly-padding rows
+  // 48..63 to the mui waves). X2_DMA_SPLIT 1: the blocks (w & 3) + 4j, j < 4, of the E part for
+  // the mui waves and of the proj and candidate parts for the X waves (which wait at the barriers).
+  // Lane l fills row 4b + (l >> 4), chunk slot l & 15 from source chunk slot ^ x2swz(row).
+  // lv bit jj: history rows of block jj live; bit 4 + jj: its candidate rows live.
+  auto dma_block = [&](int jj) { return X2_DMA_SPLIT ? (wave & 3) + 4 * jj : (jj ? 8 + (wave ^ 4) : wave); };
+  const bool dmaE = !X2_DMA_SPLIT || P == 0;
+  const bool dmaP = WEIGHTED && (!X2_DMA_SPLIT || P == 1);
+  const bool dmaC = WITH_CAND && (!X2_DMA_SPLIT || P == 1);
   auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC, unsigned& lv) {
     const int lane = threadIdx.x & 63;
     const bool live = i < n_i;
@@ -457,16 +497,16 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int U = live ? __builtin_amdgcn_readfirstlane(dup_u(smem, i & 3)[0]) : 1;
     lv = 0;
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
+    for (int jj = 0; jj < kNB; ++jj) {
       const int row0 = 4 * dma_block(jj);
-      if (live && row0 < U) lv |= 1u << jj;
-      if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 4u << jj;
+      if (live && (dmaE || dmaP) && row0 < U) lv |= 1u << jj;
+      if (live && dmaC && row0 < cnt - 64 * pass) lv |= 16u << jj;
       const int row = row0 + (lane >> 4);
       const uint32_t poff = (uint32_t)(((lane & 15) ^ x2swz(row)) << 4);
       int h = 0, c = 0;
       if (live) {
-        h = l1_his(smem, i & 3)[min(row, U - 1)];
-        if (WITH_CAND) c = l1_cand(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
+        if (dmaE || dmaP) h = l1_his(smem, i & 3)[min(row, U - 1)];
+        if (dmaC) c = l1_cand(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
       }
       h = min(max(h, 0), p.n_news - 1);
       c = min(max(c, 0), p.n_news - 1);
@@ -481,13 +521,13 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const char* bE = tabB + cc * kRB;
     const char* bP = prjB + cc * kRB;
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
+    for (int jj = 0; jj < kNB; ++jj) {
       const unsigned m = sbase + slot * kSlot + dma_block(jj) * 1024;
       if (lv & (1u << jj)) {
-        x2_dma_row(oH[jj], bE, m);
-        if constexpr (WEIGHTED) x2_dma_row(oH[jj], bP, m + kPart);
+        if (dmaE) x2_dma_row(oH[jj], bE, m);
+        if (dmaP) x2_dma_row(oH[jj], bP, m + kPart);
       }
-      if (lv & (4u << jj)) x2_dma_row(oC[jj], bE, m + 2 * kPart);
+      if (lv & (16u << jj)) x2_dma_row(oC[jj], bE, m + 2 * kPart);
     }
   };
 
@@ -521,36 +561,48 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   u32x4 aH[2], aL[2], aH1[2], aL1[2];
   // softmax over the history groups (model.py:176-181) of this wave's 16 interests, in registers:
   // lane (g, i) takes 16 groups, the 4 lane rows combined by permlanes
-  auto softmax_inwave = [&](int i, int ktile, u32x4* dH, u32x4* dL) {
+  // path pth (0: E rows, 1: proj rows) picks the units; kap = κ_k of this lane's interest
+  auto softmax_inwave = [&](int i, int ktile, int pth, u32x4* dH, u32x4* dL, float& kap) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const int k = 16 * ktile + j;
     const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
     const float* pr = prep_blk(smem, i);
-    float v[16], wm[16];
+    float v[16], wm[16], un[16];
     float mx = -INFINITY;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int u = 32 * (s >> 3) + 16 * ((s >> 2) & 1) + 4 * g + (s & 3);
       const float mu = pr[u];
-      wm[s] = fabsf(mu);
+      const int code = (int)fabsf(mu);
+      wm[s] = (float)(code & 127);
+      const int eb = pth ? (code >> 15) : ((code >> 7) & 255);
+      un[s] = __int_as_float((eb - 14) << 23);          // the row's unit 2^(eb - 141)
       v[s] = __builtin_fmaf(lgb[u * 32 + k], mu > 0.f ? 1.f : 0.f, pr[64 + u]);
       mx = fmaxf(mx, v[s]);
     }
     mx = x_rows4_max(mx);
-    float sum = 0.f;
+    float sum = 0.f, tu = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       v[s] = x2_exp(v[s] - mx);              // 0 past U (v = -inf there; weight 0)
-      sum = __builtin_fmaf(wm[s], v[s], sum);
+      const float we = wm[s] * v[s];
+      sum += we;
+      tu = __builtin_fmaf(we, un[s], tu);
     }
     sum = x_rows4_sum(sum);
-    float inv = kSA / sum;
+    tu = x_rows4_sum(tu);
+    // T_k = Σ_u A_ku·unit_u < 2^e: κ_k = 2^(14 - e) keeps every κ_k·A_ku·unit_u below 2^14
+    int e;
+    frexpf(tu / sum, &e);
+    e = min(max(e, -100), 114);
+    kap = __int_as_float((141 - e) << 23);              // 2^(14 - e)
+    float inv = kap / sum;
     if (k >= KK) inv = 0.f;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       unsigned h, l;
-      split2w(wm[2 * m], v[2 * m], wm[2 * m + 1], v[2 * m + 1], inv, h, l);
+      split2w(wm[2 * m], v[2 * m], inv * un[2 * m], wm[2 * m + 1], v[2 * m + 1], inv * un[2 * m + 1], h, l);
       dH[m >> 2][m & 3] = h;
       dL[m >> 2][m & 3] = l;
     }
@@ -570,7 +622,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   issue_L2(0); issue_L2(1);
   vm_wait_all();
   raw_barrier();
-  uint32_t cH[2], cC[2], nH[2] = {0u, 0u}, nC[2] = {0u, 0u};
+  uint32_t cH[kNB], cC[kNB], nH[kNB], nC[kNB];
+#pragma unroll
+  for (int jj = 0; jj < kNB; ++jj) nH[jj] = nC[jj] = 0u;
   unsigned cLv = 0, nLv = 0;
   item_offsets(0, 0, cH, cC, cLv);
   dma_chunk(cH, cC, cLv, 0, 0);
@@ -636,8 +690,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int o = c * 32 + ((8 * kq + j) ^ sw);
-      m[j] = (F[o] + F[2048 + o]) * m_scale;
-      if constexpr (WEIGHTED) lg[j] = (F[4096 + o] + F[6144 + o]) * lg_scale;
+      m[j] = (F[o] + F[2048 + o]) * uc_pend;                        // the candidate row's unit
+      if constexpr (WEIGHTED) lg[j] = (F[4096 + o] + F[6144 + o]) * uc_pend;
     }
     float sc;
     if constexpr (WEIGHTED) {
@@ -673,26 +727,63 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     if (kq == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
   };
 
-  // the products of one chunk in slot t & 1; mode: 1 history product, 2 candidate product, 4 mui out;
-  // NT candidate tiles compile-time
-  auto compute_t = [&](int ci, int cc, int mode, auto nt_c) {
+  // the products of one chunk in slot t & 1; mode: 1 history product, 2 candidate product, 4 mui out,
+  // 8 Gram; NT candidate tiles compile-time (0: no candidate product). Order: every LDS operand read
+  // of the chunk is issued first (asm, so hipcc neither splits them around the MFMAs nor pairs the
+  // candidate reads into conflicting ds_read2st64_b64), then the next chunk's row DMAs (`dma`),
+  // whose issue covers the reads' latency, then the history MFMAs behind a counted lgkmcnt that
+  // leaves the candidate reads in flight, the split, and the candidate MFMAs.
+  auto compute_t = [&](int ci, int cc, int mode, auto nt_c, auto&& dma) {
     constexpr int NT = decltype(nt_c)::value;
     FRESH_LANE_IDS();
     const int g = lane >> 4, i = lane & 15;
-    const char* slot = smem + (t & 1) * kSlot;
-    const char* part = slot + P * kPart;
+    const unsigned sb = sbase + (unsigned)((t & 1) * kSlot);
+    const unsigned hb = sb + (unsigned)(P * kPart);
+    const bool two = nkb == 2;        // > 32 history groups: the second 32-row block
+    uint2 rh[2][2][2], rl[2][2][2];   // [kb][ctl][rr] transposed history operand pieces (hi / lo plane)
+    // the run-time-shape eval-loss form issues the DMAs first (no spare registers across them)
+    constexpr bool kDmaFirst = LOSS && NCH == 0;
+    if constexpr (kDmaFirst) dma();
+    x2_tr_reads<0>(hb, trH, trL, rh[0], rl[0]);
+    if (!LOSS && two) x2_tr_reads<1>(hb, trH, trL, rh[1], rl[1]);   // LOSS: after block 0's MFMAs (registers)
+    constexpr int NQ = NT > 0 ? NT : 1;
+    uint2 cH_[NQ][2], cL_[NQ][2];
+    auto cand_reads = [&]() {
+#pragma unroll
+      for (int ctl = 0; ctl < 2; ++ctl) {
+        const unsigned aH = sb + cfH[ctl], aL = sb + cfL[ctl];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+          asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cH_[q][ctl]) : "v"(aH), "i"(2 * kPart + 4096 * q));
+          asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cL_[q][ctl]) : "v"(aL), "i"(2 * kPart + 4096 * q));
+        }
+      }
+    };
+    // the eval-loss form (second interest tile, Gram tiles) has no registers to spare for the
+    // candidate operands during the history product: it reads them after it
+    constexpr bool kEarly = NT > 0 && !LOSS;
+    if constexpr (kEarly) cand_reads();
+    X2_STAMP(2);
+    if constexpr (!kDmaFirst) dma();
+    X2_STAMP(3);
+    // the history reads are the oldest LDS operations in flight: all but the 4·NT candidate reads
+    constexpr int kLeave = kEarly ? (4 * NT < 15 ? 4 * NT : 15) : 0;
+    x2_tr_wait<kLeave>(rh[0], rl[0]);
+    if (!LOSS && two) x2_tr_wait<kLeave>(rh[1], rl[1]);
     f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     [[maybe_unused]] f32x4 hy[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      if (kb == 1 && nkb < 2) break;    // <= 32 unique history rows: one 32-row block
+      if (kb == 1 && !two) break;       // <= 32 unique history rows: one 32-row block
+      if (LOSS && kb == 1) {
+        x2_tr_reads<1>(hb, trH, trL, rh[1], rl[1]);
+        x2_tr_wait<0>(rh[1], rl[1]);
+      }
       u32x4 eH[2], eL[2];
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl) {
-        const uint2 h0 = lds_tr(part + trH[ctl][0] + 8192 * kb), h1 = lds_tr(part + trH[ctl][1] + 8192 * kb);
-        const uint2 l0 = lds_tr(part + trL[ctl][0] + 8192 * kb), l1 = lds_tr(part + trL[ctl][1] + 8192 * kb);
-        eH[ctl] = u32x4{h0.x, h0.y, h1.x, h1.y};
-        eL[ctl] = u32x4{l0.x, l0.y, l1.x, l1.y};
+        eH[ctl] = u32x4{rh[kb][ctl][0].x, rh[kb][ctl][0].y, rh[kb][ctl][1].x, rh[kb][ctl][1].y};
+        eL[ctl] = u32x4{rl[kb][ctl][0].x, rl[kb][ctl][0].y, rl[kb][ctl][1].x, rl[kb][ctl][1].y};
       }
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl) hx[ctl] = mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
@@ -708,10 +799,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       float y0[8], y1[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        y0[e] = hx[0][e] * op_scale;
-        y0[4 + e] = hx[1][e] * op_scale;
-        y1[e] = hy[0][e] * op_scale;
-        y1[4 + e] = hy[1][e] * op_scale;
+        y0[e] = hx[0][e] * (1.0f / kSA);       // the Gram waves are mui waves: |κ_k·mui_k| < 2^28
+        y0[4 + e] = hx[1][e] * (1.0f / kSA);
+        y1[e] = hy[0][e] * (1.0f / kSA);
+        y1[4 + e] = hy[1][e] * (1.0f / kSA);
       }
       u32x4 g0H, g0L, g1H, g1L;
       split8h(y0, g0H, g0L);
@@ -721,43 +812,19 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       gr[2] = mfma_x2(gr[2], g1H, g1L, g1H, g1L);
     }
     if ((mode & 4) && 16 * kt + i < KK) {
+      const float mui_scale = __builtin_amdgcn_rcpf(kap);   // exact: κ is a power of two
       float* dst = mui_out + ((size_t)imp_b(ci) * KK + 16 * kt + i) * d + kCW * cc + 32 * ch + 4 * g;
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl)
         *reinterpret_cast<float4*>(dst + 16 * ctl) =
             make_float4(hx[ctl][0] * mui_scale, hx[ctl][1] * mui_scale, hx[ctl][2] * mui_scale, hx[ctl][3] * mui_scale);
     }
-    if (mode & 2) {
-      uint2 cH_[NT][2], cL_[NT][2];
-#if X2_CAND_ASM
-      // plain ds_read_b64 from asm: hipcc pairs the q and q + 1 reads of one base into
-      // ds_read2st64_b64, whose 16-lane groups bank by dword mod 32, a 2-way conflict on these
-      // 16-row reads (MI355X_MICROARCH.md §LDS); ds_read_b64 banks mod 64 over 32 lanes: none.
-      // Their completion is waited for below (x2_lds_wait), before the candidate MFMAs.
-      {
-        const unsigned cb = lds_offset(slot);
-#pragma unroll
-        for (int ctl = 0; ctl < 2; ++ctl) {
-          const unsigned aH = cb + cfH[ctl], aL = cb + cfL[ctl];
-#pragma unroll
-          for (int q = 0; q < NT; ++q) {
-            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cH_[q][ctl]) : "v"(aH), "i"(2 * kPart + 4096 * q));
-            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cL_[q][ctl]) : "v"(aL), "i"(2 * kPart + 4096 * q));
-          }
-        }
-      }
-#else
-      const char* cpart = slot + 2 * kPart;
-#pragma unroll
-      for (int q = 0; q < NT; ++q) {
-#pragma unroll
-        for (int ctl = 0; ctl < 2; ++ctl) {
-          cH_[q][ctl] = lds_u64(cpart + cfH[ctl] + 4096 * q);
-          cL_[q][ctl] = lds_u64(cpart + cfL[ctl] + 4096 * q);
-        }
-      }
-#endif
+    if constexpr (NT > 0) {
+      if constexpr (!kEarly) cand_reads();
       float x[8];
+      // mui path: κ·mui·2^-14 (< 2^14); X path: the GELU's input (A·proj)_k = acc / κ, then
+      // gelu·κ·2^-14 (|gelu(y)| <= |y|)
+      const float op_scale = P == 0 ? 1.0f / kSA : __builtin_amdgcn_rcpf(kap);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         x[e] = hx[0][e] * op_scale;
@@ -765,14 +832,13 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
       if (WEIGHTED && P == 1) {
         gelu_as_pairs(x, 8);
+        const float sPj = kap * (1.0f / kSA);
 #pragma unroll
         for (int e = 0; e < 8; ++e) x[e] *= sPj;
       }
       u32x4 bH, bL;
       split8h(x, bH, bL);
-#if X2_CAND_ASM
       x2_lds_wait<NT>(cH_, cL_);
-#endif
       X2_STAMP(5);
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
@@ -783,13 +849,17 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       X2_STAMP(6);
     }
   };
-  using I4 = std::integral_constant<int, 4>;
-  auto compute = [&](int ci, int cc, int mode, int ntile) {
-    if (!(mode & 1)) return;
-    if (!(mode & 2) || ntile >= 4) compute_t(ci, cc, mode, I4{});
-    else if (ntile == 3) compute_t(ci, cc, mode, std::integral_constant<int, 3>{});
-    else if (ntile == 2) compute_t(ci, cc, mode, std::integral_constant<int, 2>{});
-    else compute_t(ci, cc, mode, std::integral_constant<int, 1>{});
+  auto compute = [&](int ci, int cc, int mode, int ntile, auto&& dma) {
+    using std::integral_constant;
+    if (!(mode & 1)) {
+      dma();
+      return;
+    }
+    if (!(mode & 2)) compute_t(ci, cc, mode, integral_constant<int, 0>{}, dma);
+    else if (ntile >= 4) compute_t(ci, cc, mode, integral_constant<int, 4>{}, dma);
+    else if (ntile == 3) compute_t(ci, cc, mode, integral_constant<int, 3>{}, dma);
+    else if (ntile == 2) compute_t(ci, cc, mode, integral_constant<int, 2>{}, dma);
+    else compute_t(ci, cc, mode, integral_constant<int, 1>{}, dma);
   };
 
   // static priority for the X waves 4-7 (the GELU chain)
@@ -823,8 +893,11 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           pend_d = -1;
           d_pending = false;
           if (cp == 0) {
-            softmax_inwave(ci, kt, aH, aL);
-            if (LOSS && gram_w && dis_out) softmax_inwave(ci, 1, aH1, aL1);
+            softmax_inwave(ci, kt, P, aH, aL, kap);
+            if (LOSS && gram_w && dis_out) {
+              float kap1;                // interest tile 1 of the Gram: the Gram's cosines are per-k scale free
+              softmax_inwave(ci, 1, 0, aH1, aL1, kap1);
+            }
             dedupe_prep(ci + 2);       // L1 of ci + 2 landed; its logit rows are DMA'd by group next
             if (nchunk == 1) {
               raw_barrier();           // every wave has read impression ci's logit rows and coefficients
@@ -838,15 +911,20 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         } else if (cc == 1 && cp == 0) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
         }
-        X2_STAMP(2);
-        if (cc + 1 < nchunk) {
-          dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
-        } else {
-          item_offsets(ni, np, nH, nC, nLv);
-          dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
-        }
-        X2_STAMP(3);
-        compute(ci, cc, mode, ntile);
+        compute(ci, cc, mode, ntile, [&]() {
+          if (cc + 1 < nchunk) {
+            dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
+          } else {
+            item_offsets(ni, np, nH, nC, nLv);
+            dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
+          }
+        });
+      }
+      if (WITH_CAND && wave >= 4) {
+        // this pass's S7 (after the next barrier) needs its candidates' row units: one per lane
+        const int c = 16 * (wave & 3) + (int)(threadIdx.x & 15);
+        const int id = l1_cand(smem, ci & 3)[min(64 * cp + min(c, max(cntp, 1) - 1), kMaxCand - 1)];
+        uc_pend = p.unit_t[min(max(id, 0), p.n_news - 1)];
       }
       if (nchunk == 1 && did_s7) raw_barrier();
       if (LOSS && dis_out && cp == 0) {
@@ -871,6 +949,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         const int lane = threadIdx.x & 63;
         const int j = lane & 15, g = lane >> 4;
         if (path_live && k_live) {
+          // in true units over the candidate row's unit: M = M_s·unit_c·2^14/κ_k (Lg likewise)
+          const float pub_scale = kSA * __builtin_amdgcn_rcpf(kap);
           float* F = reinterpret_cast<float*>(smem + kOffF) + (P * 2 + ch) * 2048;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -878,7 +958,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const int c = 16 * q + 4 * g + e;
-                F[c * 32 + ((16 * kt + j) ^ ((c >> 1) & 31))] = acc[q][e];
+                F[c * 32 + ((16 * kt + j) ^ ((c >> 1) & 31))] = acc[q][e] * pub_scale;
               }
             }
           }
@@ -886,7 +966,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
       pend_off = c_off + 64 * cp;
       pend_cnt = cntp;
-      cH[0] = nH[0]; cH[1] = nH[1]; cC[0] = nC[0]; cC[1] = nC[1]; cLv = nLv;
+#pragma unroll
+      for (int jj = 0; jj < kNB; ++jj) {
+        cH[jj] = nH[jj];
+        cC[jj] = nC[jj];
+      }
+      cLv = nLv;
     }
   }
   X2_STAMP_FLUSH(n_i);
@@ -982,35 +1067,28 @@ int miner_news_x2_debug_stage_cycles(unsigned long long* out) {
 }
 #endif
 
-size_t miner_news_x2_workspace_floats(void) { return (size_t)kAbsBlocks + 8; }
-
-int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* workspace) {
-  if (!src || !dst || !workspace || n <= 0 || d <= 0) return MINER_EINVAL;
-  if (d % 64) return MINER_ESHAPE;
-  if (!al16(src) || !al16(dst) || !al16(workspace)) return MINER_EALIGN;
+int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* row_unit) {
+  if (!src || !dst || !row_unit || n <= 0 || d <= 0) return MINER_EINVAL;
+  if (d % 64 || d > 64 * 8 * kSplitMaxG) return MINER_ESHAPE;
+  if (!al16(src) || !al16(dst)) return MINER_EALIGN;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(x2_absmax, dim3(kAbsBlocks), dim3(256), 0, s, src, (size_t)n * d, workspace + 8);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  const size_t groups = (size_t)n * (d >> 3);
-  const int grid = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
-  hipLaunchKernelGGL(x2_split, dim3(grid), dim3(256), 0, s, src, n, d, workspace + 8, static_cast<unsigned short*>(dst),
-                     workspace);
-  e = hipGetLastError();
+  const int grid = (n + 3) / 4 < 8192 ? (n + 3) / 4 : 8192;
+  hipLaunchKernelGGL(x2_split_rows, dim3(grid), dim3(256), 0, s, src, n, d, static_cast<unsigned short*>(dst), row_unit);
+  const hipError_t e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
-int miner_score_news_x2(void* stream, int score_type, const void* table2, const float* table_scale,
-                        const float* news_logits, const void* proj2, const float* proj_scale, int n_news,
+int miner_score_news_x2(void* stream, int score_type, const void* table2, const float* table_unit,
+                        const float* news_logits, const void* proj2, const float* proj_unit, int n_news,
                         const int32_t* his_ids, const uint8_t* his_mask, const float* his_bias,
                         const int32_t* cand_ids, const int32_t* cand_offsets, int B, int L, int C, int d, int K,
                         float* scores, float* user_out, float* disagree_out) {
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
-  if (!table2 || !table_scale || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
+  if (!table2 || !table_unit || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
   if (L <= 0 || d <= 0 || K <= 0) return MINER_EINVAL;
   if (L > kMaxL || K > kMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
   if ((uint64_t)n_news * (uint64_t)d * 4u > 0xffffffffull) return MINER_ESHAPE;   // 32-bit row offsets
-  if (score_type == MINER_SCORE_WEIGHTED && (!proj2 || !proj_scale)) return MINER_EINVAL;
+  if (score_type == MINER_SCORE_WEIGHTED && (!proj2 || !proj_unit)) return MINER_EINVAL;
   if (score_type != MINER_SCORE_NONE) {
     if (!scores || !cand_ids) return MINER_EINVAL;
     if (!cand_offsets && (C < 0 || C > kMaxCand)) return MINER_ESHAPE;
@@ -1019,7 +1097,7 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
   }
   if (!al16(table2) || !al16(news_logits) || !al16(proj2)) return MINER_EALIGN;
   if (B == 0) return MINER_OK;
-  X2Params prm{table2, news_logits, proj2, table_scale, proj_scale ? proj_scale : table_scale, his_ids, his_mask, his_bias,
+  X2Params prm{table2, news_logits, proj2, table_unit, proj_unit ? proj_unit : table_unit, his_ids, his_mask, his_bias,
                score_type == MINER_SCORE_NONE ? nullptr : cand_ids,
                score_type == MINER_SCORE_NONE ? nullptr : cand_offsets,
                scores, user_out, disagree_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type};

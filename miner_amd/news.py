@@ -35,11 +35,12 @@ MAX_CAND = 512          # MINER_NEWS_MAX_CAND: candidates per impression
 @dataclasses.dataclass
 class PairPlanes:
     """fp32 tables as exact-sum fp16 pairs (miner_news_split_x2): the operands of the fp32 scoring
-    kernel on the fp16 matrix cores (news_x2.hip). Same bytes as fp32; ``*_ws`` hold the scale."""
+    kernel on the fp16 matrix cores (news_x2.hip). Same bytes as fp32; row r holds x / unit[r], one
+    power-of-two unit per row (``*_unit``)."""
     table2: Tensor                # [n_news, 2d] fp16 (per 64-column chunk: 64 hi | 64 lo)
-    table_ws: Tensor              # fp32 workspace, [0] = scale, [1] = 1/scale
+    table_unit: Tensor            # [n_news] fp32 row units
     proj2: Optional[Tensor]
-    proj_ws: Optional[Tensor]
+    proj_unit: Optional[Tensor]
 
 
 @dataclasses.dataclass
@@ -87,8 +88,8 @@ def x2_fits(n_news: int, d: int) -> bool:
     return n_news * d * 4 <= 0xFFFFFFFF
 
 
-def split_x2(src: Tensor, out: Optional[Tensor] = None, ws: Optional[Tensor] = None):
-    """fp32 [n, d] -> (pairs [n, 2d] fp16, workspace with the scale) (miner_news_split_x2)."""
+def split_x2(src: Tensor, out: Optional[Tensor] = None, unit: Optional[Tensor] = None):
+    """fp32 [n, d] -> (pairs [n, 2d] fp16, row units [n] fp32) (miner_news_split_x2)."""
     _require_device(src)
     src = _contig(src)
     if src.dtype != torch.float32 or src.dim() != 2:
@@ -96,13 +97,12 @@ def split_x2(src: Tensor, out: Optional[Tensor] = None, ws: Optional[Tensor] = N
     n, d = src.shape
     if out is None or tuple(out.shape) != (n, 2 * d):
         out = torch.empty((n, 2 * d), device=src.device, dtype=torch.float16)
-    nws = int(_lib.lib().miner_news_x2_workspace_floats())
-    if ws is None or ws.numel() < nws:
-        ws = torch.empty((nws,), device=src.device, dtype=torch.float32)
+    if unit is None or unit.numel() != n:
+        unit = torch.empty((n,), device=src.device, dtype=torch.float32)
     with torch.cuda.device(src.device):
-        rc = _lib.lib().miner_news_split_x2(_stream(src.device), _ptr(src), n, d, _ptr(out), _ptr(ws))
+        rc = _lib.lib().miner_news_split_x2(_stream(src.device), _ptr(src), n, d, _ptr(out), _ptr(unit))
     _lib.check(rc, "miner_news_split_x2")
-    return out, ws
+    return out, unit
 
 
 def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = None,
@@ -147,8 +147,8 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
         want_x2 = False
     if want_x2:
         o = out.x2 if out is not None and out.x2 is not None else None
-        t2, tws = split_x2(table, None if o is None else o.table2, None if o is None else o.table_ws)
-        p2, pws = (split_x2(proj, None if o is None else o.proj2, None if o is None else o.proj_ws)
+        t2, tws = split_x2(table, None if o is None else o.table2, None if o is None else o.table_unit)
+        p2, pws = (split_x2(proj, None if o is None else o.proj2, None if o is None else o.proj_unit)
                    if proj is not None else (None, None))
         planes = PairPlanes(t2, tws, p2, pws)
     return NewsTable(table, logits, proj, pw.K, planes)
@@ -234,8 +234,8 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
     with torch.cuda.device(dev):
         if use_x2:
             px = nt.x2
-            rc = _lib.lib().miner_score_news_x2(_stream(dev), st, _ptr(px.table2), _ptr(px.table_ws), _ptr(nt.logits),
-                                                _ptr(px.proj2), _ptr(px.proj_ws), nt.n_news, _ptr(hid), _ptr(mask),
+            rc = _lib.lib().miner_score_news_x2(_stream(dev), st, _ptr(px.table2), _ptr(px.table_unit), _ptr(nt.logits),
+                                                _ptr(px.proj2), _ptr(px.proj_unit), nt.n_news, _ptr(hid), _ptr(mask),
                                                 _ptr(his_bias), _ptr(cid), _ptr(offs), B, L, C, d, K, _ptr(scores),
                                                 _ptr(mui), _ptr(dis))
         else:

@@ -147,3 +147,44 @@ def test_config5_bench_step_fp32():
     sub = torch.tensor(users, device=DEV)
     s2, i2 = corpus.rank_topk(mui[sub], proj[sub], table, topk)
     assert torch.equal(s2, top_s[sub]) and torch.equal(i2, top_i[sub])
+
+
+def test_config5_bench_step_fp16():
+    """The bench's config-5 step in its BASELINE dtype (fp16): 2,048 users (L=200, K=64) against a
+    200,000-news fp16 table with the fused top-100. Sampled users' lists against the oracle's full
+    200k scores computed from the kernel's own 16-bit user vectors and the fp16 table (the ranker's
+    arithmetic: fp16 operands, fp32 accumulation; RANK16_TOL of tests/test_gpu_corpus.py), no news
+    outside a list above its last entry, and batch independence (users ranked alone: same lists)."""
+    from miner_amd import corpus
+    from oracle import corpus_oracle as co
+    U, L, K, N, d, topk = 2048, 200, 64, 200_000, 768, 100
+    rtol = rms_floor = 2e-4
+    g = torch.Generator(device=DEV).manual_seed(5)
+    table = (torch.randn((N, d), generator=g, device=DEV) / d ** 0.5).to(torch.float16)
+    W1, Q, W2 = synthetic.init_weights(5, d, 200, K, device=DEV)
+    pk = corpus.pack_encoder(W1, Q, W2, dtype=torch.float16)
+    hid = torch.randint(0, N, (U, L), generator=g, device=DEV, dtype=torch.int32)
+    lens = torch.randint(1, L + 1, (U,), generator=g, device=DEV)
+    mask = torch.arange(L, device=DEV)[None, :] >= (L - lens)[:, None]
+    mui, proj = corpus.encode_users(table, mask, pk, his_ids=hid)
+    top_s, top_i = corpus.rank_topk(mui, proj, table, topk)
+    torch.cuda.synchronize()
+    assert mui.dtype == torch.float16 and torch.isfinite(top_s).all() and bool((top_i >= 0).all())
+    users = [0, 1, 777, 1500, 2047]
+    T = table.float().cpu()
+    with torch.no_grad():
+        full = co.corpus_scores(mui[users].float().cpu(), proj[users].float().cpu(), T)   # [5, N] fp32
+    rms = float(full.pow(2).mean().sqrt())
+    for r, u in enumerate(users):
+        got_i = top_i[u].cpu().long()
+        assert len(set(got_i.tolist())) == topk
+        true = full[r, got_i].double()
+        err = (top_s[u].cpu().double() - true).abs()
+        assert bool((err <= rtol * true.abs() + rms_floor * rms).all()), (u, float(err.max()))
+        kth = float(true.min())
+        outside = torch.ones(N, dtype=torch.bool)
+        outside[got_i] = False
+        assert float(full[r, outside].max()) <= kth + rms_floor * rms + rtol * abs(kth), u
+    sub = torch.tensor(users, device=DEV)
+    s2, i2 = corpus.rank_topk(mui[sub], proj[sub], table, topk)
+    assert torch.equal(s2, top_s[sub]) and torch.equal(i2, top_i[sub])

@@ -187,6 +187,30 @@ def _heavy_tailed(seed, B=240, L=50, d=768, n_news=4000, C=40):
     return t.to(DEV), hid.to(DEV), mask.to(DEV), cid.to(DEV), W1, Q, W2
 
 
+def test_x2_split_rows_exact_sum():
+    """miner_news_split_x2: every row r is (hi + lo)·unit[r] with unit[r] a power of two and
+    max|row| / unit[r] in [2^13, 2^14); each element within 2^-22 of itself (2^-24·unit absolute
+    where lo falls below the fp16 normals), whatever the magnitude of the other rows."""
+    table, *_ = _heavy_tailed(36, n_news=600, d=256)
+    table[7] = 0.0                                    # an all-zero row
+    table[8] *= 1e-20                                 # a tiny row
+    t2, unit = news.split_x2(table)
+    torch.cuda.synchronize()
+    t2, unit, x = t2.cpu().float(), unit.cpu().double(), table.cpu().double()
+    n, d = x.shape
+    pl = t2.view(n, d // 64, 2, 64)
+    back = (pl[:, :, 0, :].double() + pl[:, :, 1, :].double()).reshape(n, d) * unit[:, None]
+    m = x.abs().max(dim=1).values
+    e = torch.log2(unit)
+    assert torch.equal(e, e.round()), "units are powers of two"
+    nz = m > 0
+    ratio = m[nz] / unit[nz]
+    assert bool(((ratio >= 2 ** 13) & (ratio < 2 ** 14)).all()), ratio
+    err = (back - x).abs()
+    bound = torch.maximum(x.abs() * 2.0 ** -22, unit[:, None] * 2.0 ** -24)
+    assert bool((err <= bound).all()), float((err / bound).max())
+
+
 @pytest.mark.parametrize("score_type", ["max", "weighted"])
 def test_x2_heavy_tailed(score_type, monkeypatch):
     """Heavy-tailed tables (rows 1e4x and 1e5x the median norm, a few dimensions 100x the rest):

@@ -1,6 +1,8 @@
 """Run the news-path scoring kernel `reps` times at config-3 shape (for rocprofv3 passes).
 
-    python tools/news_once.py [fp32|bf16] [B] [reps] [d] [n_news]
+    python tools/news_once.py [fp32|bf16] [B] [reps] [d] [n_news] [full]
+
+``full``: every history holds L clicks (the bench's full_histories sub-line).
 
 fp32 runs the fp16-pair kernel news_score_x2 unless MINER_NEWS_FP32=mfma32 (news_score32). d = 256
 with n_news = 65238 is config 2.
@@ -22,7 +24,8 @@ n_news = int(sys.argv[5]) if len(sys.argv) > 5 else 104000
 L, C, K, Dc = 50, 40, 32, 200
 g = torch.Generator(device=dev).manual_seed(36)
 table = (torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5).to(dt)
-lens = torch.randint(0, L + 1, (B,), generator=g, device=dev)
+full = len(sys.argv) > 6 and sys.argv[6] == "full"
+lens = torch.full((B,), L, device=dev) if full else torch.randint(0, L + 1, (B,), generator=g, device=dev)
 mask = torch.arange(L, device=dev)[None, :] >= (L - lens)[:, None]
 hid = torch.randint(1, n_news, (B, L), generator=g, device=dev, dtype=torch.int32)
 hid[~mask] = 0

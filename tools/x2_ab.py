@@ -59,8 +59,8 @@ def run(names, B=1_000_000, reps=5):
 
     def launch(n):
         px = nt.x2
-        rc = libs[n].miner_score_news_x2(st, 0, px.table2.data_ptr(), px.table_ws.data_ptr(), nt.logits.data_ptr(),
-                                         px.proj2.data_ptr(), px.proj_ws.data_ptr(), n_news, beh.his_ids.data_ptr(),
+        rc = libs[n].miner_score_news_x2(st, 0, px.table2.data_ptr(), px.table_unit.data_ptr(), nt.logits.data_ptr(),
+                                         px.proj2.data_ptr(), px.proj_unit.data_ptr(), n_news, beh.his_ids.data_ptr(),
                                          mask.data_ptr(), None, beh.cand_ids.data_ptr(), None, B, L, C, d, K,
                                          out[n].data_ptr(), None, dis[n].data_ptr() if loss else None)
         assert rc == 0, rc

@@ -58,7 +58,7 @@ bi = bad.sum((1, 2))
 print("impressions with bad elems:", int((bi > 0).sum()), "lens of those:", sorted(lens_c[bi > 0].tolist())[:40])
 print("lens of clean:", sorted(lens_c[bi == 0].tolist())[:60])
 # representation check: hi/lo split of E and A in f64
-sE = float(nt.x2.table_ws[0])
+sE = float(nt.x2.table_unit[0])
 Es = T * sE
 Eh = Es.float().half().double()
 El = (Es - Eh).float().half().double()
