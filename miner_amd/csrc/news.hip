@@ -94,6 +94,23 @@ __device__ __forceinline__ float rows4_sum(float x) {
 __device__ __forceinline__ uint32_t lds_u32(const char* p) { return *reinterpret_cast<const uint32_t*>(p); }
 __device__ __forceinline__ u32x4 lds_u32x4(const char* p) { return *reinterpret_cast<const u32x4*>(p); }
 
+#ifndef NS_D256_CW128
+#define NS_D256_CW128 0
+#endif
+#ifndef NS_EARLY
+#define NS_EARLY 0       // 1: operand reads issued before the chunk's row DMAs (measured 25 % slower at d = 768)
+#endif
+// wait until at most N LDS operations are in flight, the 4 transposed pieces of a slab tied to it
+template <int N>
+__device__ __forceinline__ void ns_wait_tr(uint2 (&r)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : "i"(N));
+}
+template <int NT>
+__device__ __forceinline__ void ns_wait_c(u32x4 (&c)[NT][2]) {
+  if constexpr (NT == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c[0][0]), "+v"(c[0][1]));
+  else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c[0][0]), "+v"(c[0][1]), "+v"(c[1][0]), "+v"(c[1][1]));
+}
+
 // LDS-DMA of 16 bytes per lane with the default cache policy (table rows may be re-read by other
 // impressions: keep them in L2 / the Infinity Cache)
 __device__ __forceinline__ void dma_b128_c(const void* g, unsigned lds) {
@@ -646,7 +663,9 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   const int KK = SHP == 1 ? 32 : p.K;
   const int nchunk = NCH > 0 ? NCH : d / CW;
   // cooperative softmax one impression ahead (always for 128-column chunks: the host picks them for d >= 512)
-  const bool coop = CW == 128 || (nchunk >= PD + 1 && nchunk >= 4);
+  // (its two phases ride on chunks 1 and 2: 128-column chunks with fewer than 3 chunks per row, d = 256,
+  // compute A in-wave)
+  const bool coop = (CW == 128 && nchunk >= 3) || (nchunk >= PD + 1 && nchunk >= 4);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int w4 = SWAP ? (wave ^ 4) : wave;
   const char* tabB = static_cast<const char*>(p.table);
@@ -1055,6 +1074,85 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
   auto chunk = [&](int ci, int cc, int mode, int ncand, const uint32_t* iH, const uint32_t* iC, unsigned iLv,
                    int ich) {
     NS_STAMP(2);
+    if constexpr (sizeof(T) == 2 && NS_EARLY) {
+      // every LDS operand read of the chunk first (asm: issued together, not split around the
+      // MFMAs), then the row DMAs PD chunks ahead, whose issue covers the reads' latency, then the
+      // products behind counted lgkmcnt waits (the history reads are the oldest in flight)
+      const unsigned sb = sbase + (unsigned)((t & (NS - 1)) * Cf::SLOT);
+      const unsigned hb = sb + (unsigned)(P * Cf::PART);
+      const bool do_x = mode & 1, do_c = (mode & 3) == 3;
+      const bool two_sl = !one_slab, two_t = NT == 2 && ncand > 32;
+      uint2 tr[2][4];
+      u32x4 cf_[NT][2];
+      if (do_x) {
+#pragma unroll
+        for (int su = 0; su < 4; ++su)
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(tr[0][su]) : "v"(hb + trOff[su]));
+        if (two_sl) {
+#pragma unroll
+          for (int su = 0; su < 4; ++su)
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(tr[1][su]) : "v"(hb + trOff[4 + su]));
+        }
+        if (do_c) {
+#pragma unroll
+          for (int tl = 0; tl < NT; ++tl) {
+            if (tl == 0 || two_t) {
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                asm volatile("ds_read_b128 %0, %1" : "=v"(cf_[tl][q]) : "v"(sb + 2 * Cf::PART + cOff[tl][q]));
+            }
+          }
+        }
+      }
+      dma_chunk<T, CW, SKIP, WEIGHTED>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
+                                       sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024, iLv, (w4 + 8 - wave) * 1024);
+      NS_STAMP(3);
+      if (!do_x) return;
+      FRESH_LANE_IDS();
+      if (!do_c) ns_wait_tr<0>(tr[0]);
+      else if (two_t) ns_wait_tr<4>(tr[0]);
+      else ns_wait_tr<2>(tr[0]);
+      if (two_sl) {                    // younger than slab 0's reads: covered by the same count
+        if (!do_c) ns_wait_tr<0>(tr[1]);
+        else if (two_t) ns_wait_tr<4>(tr[1]);
+        else ns_wait_tr<2>(tr[1]);
+      }
+      f32x16 ax = zero16();
+#pragma unroll
+      for (int ls = 0; ls < 2; ++ls) {
+        if (ls == 1 && !two_sl) break;
+        Frag<T> ef;
+#pragma unroll
+        for (int su = 0; su < 4; ++su) {
+          ef.q[su >> 1][2 * (su & 1)] = tr[ls][su].x;
+          ef.q[su >> 1][2 * (su & 1) + 1] = tr[ls][su].y;
+        }
+        mma_slab(ax, ef, af[ls]);
+      }
+      NS_STAMP(4);
+      if ((mode & 4) && r < KK) {
+        float* dst = p.mui_out + ((size_t)imp_b(ci) * KK + r) * d + CW * cc + 32 * sl + 16 * h;
+#pragma unroll
+        for (int e = 0; e < 16; e += 4) *reinterpret_cast<float4*>(dst + e) = make_float4(ax[e], ax[e + 1], ax[e + 2], ax[e + 3]);
+      }
+      if (do_c) {
+        if (WEIGHTED && P == 1) gelu_tile<T>(ax);
+        Frag<T> xf;
+        acc_to_frag<T>(xf, ax);
+        NS_STAMP(5);
+        ns_wait_c<NT>(cf_);
+#pragma unroll
+        for (int tl = 0; tl < NT; ++tl) {
+          if (tl == 0 || two_t) {
+            Frag<T> cf;
+            cf.q[0] = cf_[tl][0];
+            cf.q[1] = cf_[tl][1];
+            mma_slab(acc[tl], cf, xf);
+          }
+        }
+      }
+      return;
+    }
     dma_chunk<T, CW, SKIP, WEIGHTED>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
                                      sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024, iLv, (w4 + 8 - wave) * 1024);
     NS_STAMP(3);
@@ -1137,7 +1235,7 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
           if (cp == 0) {
             if (coop) {
               load_af(ci);
-            } else if constexpr (CW == 64) {
+            } else {
               softmax_inwave(ci);
               dedupe_prep(ci + 2);
               raw_barrier();           // every wave has read impression ci's logit rows; ci + 2 grouped
@@ -2027,7 +2125,11 @@ int launch_score(void* stream, const NsParams& prm) {
       if (prm.d == 768 && !rt) { NEWS_PICK_N(1, 128, 6) }
       else { NEWS_PICK(1, 128) }       // 128-column chunks, double-buffered
     } else if (prm.d == 256 && !rt) {  // config 2
+#if NS_D256_CW128                      // A/B: 128-column chunks (2 per row), double-buffered
+      if (mind && NS_D256_CW128 == 2) { NEWS_PICK_NS(1, 128, 2, 1) } else { NEWS_PICK_N(1, 128, 2) }
+#else
       if (mind) { NEWS_PICK_NS(3, 64, 4, 1) } else { NEWS_PICK_N(3, 64, 4) }
+#endif
     } else if (nchunk >= 3) {
       NEWS_PICK(3, 64)
     } else if (nchunk == 2) {

@@ -57,10 +57,7 @@
 
 namespace {
 
-#ifndef X2_DMA_SPLIT
-#define X2_DMA_SPLIT 0
-#endif
-constexpr int kNB = X2_DMA_SPLIT ? 4 : 2;              // row-DMA blocks per wave per part
+constexpr int kNB = 2;                                 // row-DMA blocks per wave per part
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kMaxL = 64;
@@ -69,7 +66,14 @@ constexpr int kMaxCand = MINER_NEWS_MAX_CAND;
 constexpr int kCW = 64;                                // columns per chunk
 constexpr int kRB = 256;                               // bytes per staged row piece (hi | lo)
 constexpr int kPart = 64 * kRB;                        // 64 rows: E[his] | proj[his] | Cand
-constexpr int kSlot = 3 * kPart;
+// the candidate part's 16-row tiles are kCTile apart (16 B of padding after each): the reads of
+// tiles q and q + 1 from one base register are then neither a ds_read2_b64 (offsets <= 2040 B)
+// nor a ds_read2st64_b64 (multiples of 512 B) pair, which hipcc would otherwise form and whose
+// 16-lane groups bank by dword mod 32 — a 2-way conflict on these 16-row reads
+// (MI355X_MICROARCH.md §LDS); ds_read_b64 banks mod 64 over 32 lanes: none
+constexpr int kCTile = 16 * kRB + 16;
+constexpr int kCPart = 4 * kCTile;
+constexpr int kSlot = 2 * kPart + kCPart;
 constexpr float kSA = 16384.0f;                        // scale of the attention weights (A <= 1)
 
 // LDS carve (bytes): [ring x2 | F (pass partials) | logit blocks x2 | aux L1 x4 | aux L0 x8 | prep x2]
@@ -152,7 +156,13 @@ __device__ __forceinline__ void split2(float x0, float x1, unsigned& hi, unsigne
   unsigned hb = __builtin_bit_cast(unsigned, h);
   asm volatile("" : "+v"(hb));
   const f16x2 hh = __builtin_bit_cast(f16x2, hb);
-  const f16x2 l = {(_Float16)(x0 - (float)hh[0]), (_Float16)(x1 - (float)hh[1])};
+  // x - hi (exact) with hi read as an f16 half of the packed register: v_fma_mix_f32, no separate
+  // v_cvt_f32_f16 (bit-identical; -0.9 % on the x2 kernel)
+  float r0, r1;
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r0) : "v"(hb), "v"(x0));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1) : "v"(hb), "v"(x1));
+  (void)hh;
+  const f16x2 l = {(_Float16)r0, (_Float16)r1};
   hi = hb;
   lo = __builtin_bit_cast(unsigned, l);
 }
@@ -196,46 +206,6 @@ __device__ __forceinline__ float x2_exp(float x) {
   return __builtin_fmaf(e, yl * 0.69314718055994531f, e);
 }
 
-// the transposed history operand pieces of 32-row block KB (8 ds_read_b64_tr_b16 from asm): lane
-// offsets trH / trL (hi / lo plane) from the history part's LDS address hb
-template <int KB>
-__device__ __forceinline__ void x2_tr_reads(unsigned hb, const uint32_t (&trH)[2][2], const uint32_t (&trL)[2][2],
-                                            uint2 (&rh)[2][2], uint2 (&rl)[2][2]) {
-#pragma unroll
-  for (int ctl = 0; ctl < 2; ++ctl) {
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(rh[ctl][rr]) : "v"(hb + trH[ctl][rr]), "i"(8192 * KB));
-      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(rl[ctl][rr]) : "v"(hb + trL[ctl][rr]), "i"(8192 * KB));
-    }
-  }
-}
-// wait until at most N LDS operations are in flight, the 8 history pieces tied to the wait
-template <int N>
-__device__ __forceinline__ void x2_tr_wait(uint2 (&rh)[2][2], uint2 (&rl)[2][2]) {
-  asm volatile("s_waitcnt lgkmcnt(%8)" : "+v"(rh[0][0]), "+v"(rh[0][1]), "+v"(rh[1][0]), "+v"(rh[1][1]),
-               "+v"(rl[0][0]), "+v"(rl[0][1]), "+v"(rl[1][0]), "+v"(rl[1][1]) : "i"(N));
-}
-// wait for the LDS reads issued from asm into r / s (lgkmcnt(0)), the registers tied to the wait so
-// that no use moves above it
-template <int NT>
-__device__ __forceinline__ void x2_lds_wait(uint2 (&r)[NT][2], uint2 (&s)[NT][2]) {
-  if constexpr (NT == 1) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]));
-  } else if constexpr (NT == 2) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]),
-                 "+v"(r[1][0]), "+v"(r[1][1]), "+v"(s[1][0]), "+v"(s[1][1]));
-  } else if constexpr (NT == 3) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]),
-                 "+v"(r[1][0]), "+v"(r[1][1]), "+v"(s[1][0]), "+v"(s[1][1]),
-                 "+v"(r[2][0]), "+v"(r[2][1]), "+v"(s[2][0]), "+v"(s[2][1]));
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(s[0][0]), "+v"(s[0][1]),
-                 "+v"(r[1][0]), "+v"(r[1][1]), "+v"(s[1][0]), "+v"(s[1][1]),
-                 "+v"(r[2][0]), "+v"(r[2][1]), "+v"(s[2][0]), "+v"(s[2][1]),
-                 "+v"(r[3][0]), "+v"(r[3][1]), "+v"(s[3][0]), "+v"(s[3][1]));
-  }
-}
 __device__ __forceinline__ uint2 lds_tr(const char* p) {
   return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds_char*)p));
 }
@@ -437,16 +407,27 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // (first-occurrence order) and writes each group's coefficients (±m, add): s_u = logit + bias with
   // weight m for a click (+m), s_u = 1e-30 with weight m for a pad slot (-m; model.py:176-180),
   // (0, -inf) past U — and U.
+  // The groups' row units: loaded by one dedupe_prep call, merged into the codes by the next one (an
+  // impression later: the loads have landed, nothing waits on them; the codes are read two
+  // impressions after their dedupe). Wave 7 only; du_i = the impression whose units are pending.
+  float du_E = 1.f, du_P = 1.f;
+  int du_slot = -1, du_i = -1;
   auto dedupe_prep = [&](int i) {
-    if (wave != 7 || i >= n_i) return;
+    if (wave != 7) return;
     const int l = threadIdx.x & 63;
+    if (du_i >= 0) {
+      int* pcp = reinterpret_cast<int*>(prep_blk(smem, du_i));
+      if (du_slot >= 0)
+        pcp[du_slot] |= (((__float_as_int(du_E) >> 23) & 255) << 8) | (((__float_as_int(du_P) >> 23) & 255) << 16);
+      du_i = -1;
+    }
+    if (i >= n_i) return;
     int* his = l1_his(smem, i & 3);
     const int ls = min(l, L - 1);
     const int id = his[ls];
-    // the rows' units (biased exponents eb = e + 127 of unit = 2^(e - 14)), loaded now, used below
     const int idc = min(max(id, 0), p.n_news - 1);
-    const float uE = p.unit_t[idc];
-    const float uP = WEIGHTED ? p.unit_p[idc] : 1.0f;
+    du_E = p.unit_t[idc];
+    du_P = WEIGHTED ? p.unit_p[idc] : 1.0f;
     const uint32_t mw = l1_mask(smem, i & 3)[ls];
     const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + ls) & 3);
     const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
@@ -463,31 +444,30 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int U = __popcll(bal);
     const int uidx = __popcll(bal & ((1ull << l) - 1ull));
     float* pr = prep_blk(smem, i);
-    // (±code, add): the sign says click / pad; |code| = m + 128·ebE + 32768·ebP (< 2^24, exact):
-    // the multiplicity and the two rows' unit exponents
-    const int ebE = ((__float_as_int(uE) >> 23) & 255) + 14, ebP = ((__float_as_int(uP) >> 23) & 255) + 14;
+    // (code, add) per group; code, an integer: bits 0-7 the multiplicity m, 8-15 / 16-23 the
+    // exponent fields of the E / proj rows' units (powers of two; or'ed in by the next call), bit
+    // 24 set for a click
+    int* pc = reinterpret_cast<int*>(pr);
     if (uniq) {
       his[uidx] = id;
-      const float code = (float)(m + 128 * ebE + 32768 * ebP);
-      pr[uidx] = keep ? code : -code;
+      pc[uidx] = m | (keep ? 1 << 24 : 0);
       pr[64 + uidx] = keep ? bv : 1e-30f;
     }
     if (l >= U) {                        // every coefficient past the groups (a unique lane may sit there):
-      pr[l] = (float)(128 * 127 + 32768 * 127);   // m = 0, units 2^-14
+      pc[l] = (113 << 8) | (113 << 16);  // m = 0, units 2^-14
       pr[64 + l] = -INFINITY;
     }
     if (l == 0) dup_u(smem, i & 3)[0] = U;
+    du_slot = uniq ? uidx : -1;
+    du_i = i;
   };
-  // row DMAs of a chunk. X2_DMA_SPLIT 0: wave w issues the 4-row blocks w and 8 + (w ^ 4) of every
-  // part (the rows 32..47, live for L = 50 / C = 40, go to the X waves, the mostly-padding rows
-  // 48..63 to the mui waves). X2_DMA_SPLIT 1: the blocks (w & 3) + 4j, j < 4, of the E part for
-  // the mui waves and of the proj and candidate parts for the X waves (which wait at the barriers).
-  // Lane l fills row 4b + (l >> 4), chunk slot l & 15 from source chunk slot ^ x2swz(row).
+  // row DMAs of a chunk: wave w issues the 4-row blocks w and 8 + (w ^ 4) of every part (the rows
+  // 32..47, live for L = 50 / C = 40, go to the X waves, the mostly-padding rows 48..63 to the mui
+  // waves; all E rows on the mui waves and all proj / candidate rows on the X waves measured 10 %
+  // slower). Lane l fills row 4b + (l >> 4), chunk slot l & 15 from source chunk slot ^ x2swz(row).
   // lv bit jj: history rows of block jj live; bit 4 + jj: its candidate rows live.
-  auto dma_block = [&](int jj) { return X2_DMA_SPLIT ? (wave & 3) + 4 * jj : (jj ? 8 + (wave ^ 4) : wave); };
-  const bool dmaE = !X2_DMA_SPLIT || P == 0;
-  const bool dmaP = WEIGHTED && (!X2_DMA_SPLIT || P == 1);
-  const bool dmaC = WITH_CAND && (!X2_DMA_SPLIT || P == 1);
+  auto dma_block = [&](int jj) { return jj ? 8 + (wave ^ 4) : wave; };
+  constexpr bool dmaE = true, dmaP = WEIGHTED, dmaC = WITH_CAND;
   auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC, unsigned& lv) {
     const int lane = threadIdx.x & 63;
     const bool live = i < n_i;
@@ -527,7 +507,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         if (dmaE) x2_dma_row(oH[jj], bE, m);
         if (dmaP) x2_dma_row(oH[jj], bP, m + kPart);
       }
-      if (lv & (16u << jj)) x2_dma_row(oC[jj], bE, m + 2 * kPart);
+      if (lv & (16u << jj)) x2_dma_row(oC[jj], bE, m + 2 * kPart + (dma_block(jj) >> 2) * 16);
     }
   };
 
@@ -559,6 +539,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kt + i][u] of the history
   // groups u = 32 kb + 16 (e >> 2) + 4g + (e & 3) (aH1 / aL1: interest tile 1, the Gram waves only)
   u32x4 aH[2], aL[2], aH1[2], aL1[2];
+
   // softmax over the history groups (model.py:176-181) of this wave's 16 interests, in registers:
   // lane (g, i) takes 16 groups, the 4 lane rows combined by permlanes
   // path pth (0: E rows, 1: proj rows) picks the units; kap = κ_k of this lane's interest
@@ -568,17 +549,18 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int k = 16 * ktile + j;
     const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
     const float* pr = prep_blk(smem, i);
+    const int* pc = reinterpret_cast<const int*>(pr);
+    const unsigned sh = pth ? 16u : 8u;
     float v[16], wm[16], un[16];
     float mx = -INFINITY;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int u = 32 * (s >> 3) + 16 * ((s >> 2) & 1) + 4 * g + (s & 3);
-      const float mu = pr[u];
-      const int code = (int)fabsf(mu);
-      wm[s] = (float)(code & 127);
-      const int eb = pth ? (code >> 15) : ((code >> 7) & 255);
-      un[s] = __int_as_float((eb - 14) << 23);          // the row's unit 2^(eb - 141)
-      v[s] = __builtin_fmaf(lgb[u * 32 + k], mu > 0.f ? 1.f : 0.f, pr[64 + u]);
+      const unsigned code = (unsigned)pc[u];
+      wm[s] = (float)(code & 255u);
+      un[s] = __uint_as_float(__builtin_amdgcn_ubfe(code, sh, 8) << 23);     // the row's unit
+      const float click = __uint_as_float((code >> 24) * 0x3f800000u);         // 1 for a click, else 0
+      v[s] = __builtin_fmaf(lgb[u * 32 + k], click, pr[64 + u]);
       mx = fmaxf(mx, v[s]);
     }
     mx = x_rows4_max(mx);
@@ -727,63 +709,27 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     if (kq == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
   };
 
-  // the products of one chunk in slot t & 1; mode: 1 history product, 2 candidate product, 4 mui out,
-  // 8 Gram; NT candidate tiles compile-time (0: no candidate product). Order: every LDS operand read
-  // of the chunk is issued first (asm, so hipcc neither splits them around the MFMAs nor pairs the
-  // candidate reads into conflicting ds_read2st64_b64), then the next chunk's row DMAs (`dma`),
-  // whose issue covers the reads' latency, then the history MFMAs behind a counted lgkmcnt that
-  // leaves the candidate reads in flight, the split, and the candidate MFMAs.
-  auto compute_t = [&](int ci, int cc, int mode, auto nt_c, auto&& dma) {
+  // the products of one chunk in slot t & 1 (after the next chunk's row DMAs, issued first so that
+  // they land before the next barrier); mode: 1 history product, 2 candidate product, 4 mui out,
+  // 8 Gram; NT candidate tiles compile-time (0: no candidate product)
+  auto compute_t = [&](int ci, int cc, int mode, auto nt_c) {
     constexpr int NT = decltype(nt_c)::value;
     FRESH_LANE_IDS();
     const int g = lane >> 4, i = lane & 15;
-    const unsigned sb = sbase + (unsigned)((t & 1) * kSlot);
-    const unsigned hb = sb + (unsigned)(P * kPart);
-    const bool two = nkb == 2;        // > 32 history groups: the second 32-row block
-    uint2 rh[2][2][2], rl[2][2][2];   // [kb][ctl][rr] transposed history operand pieces (hi / lo plane)
-    // the run-time-shape eval-loss form issues the DMAs first (no spare registers across them)
-    constexpr bool kDmaFirst = LOSS && NCH == 0;
-    if constexpr (kDmaFirst) dma();
-    x2_tr_reads<0>(hb, trH, trL, rh[0], rl[0]);
-    if (!LOSS && two) x2_tr_reads<1>(hb, trH, trL, rh[1], rl[1]);   // LOSS: after block 0's MFMAs (registers)
-    constexpr int NQ = NT > 0 ? NT : 1;
-    uint2 cH_[NQ][2], cL_[NQ][2];
-    auto cand_reads = [&]() {
-#pragma unroll
-      for (int ctl = 0; ctl < 2; ++ctl) {
-        const unsigned aH = sb + cfH[ctl], aL = sb + cfL[ctl];
-#pragma unroll
-        for (int q = 0; q < NT; ++q) {
-          asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cH_[q][ctl]) : "v"(aH), "i"(2 * kPart + 4096 * q));
-          asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(cL_[q][ctl]) : "v"(aL), "i"(2 * kPart + 4096 * q));
-        }
-      }
-    };
-    // the eval-loss form (second interest tile, Gram tiles) has no registers to spare for the
-    // candidate operands during the history product: it reads them after it
-    constexpr bool kEarly = NT > 0 && !LOSS;
-    if constexpr (kEarly) cand_reads();
-    X2_STAMP(2);
-    if constexpr (!kDmaFirst) dma();
-    X2_STAMP(3);
-    // the history reads are the oldest LDS operations in flight: all but the 4·NT candidate reads
-    constexpr int kLeave = kEarly ? (4 * NT < 15 ? 4 * NT : 15) : 0;
-    x2_tr_wait<kLeave>(rh[0], rl[0]);
-    if (!LOSS && two) x2_tr_wait<kLeave>(rh[1], rl[1]);
+    const char* slot = smem + (t & 1) * kSlot;
+    const char* part = slot + P * kPart;
     f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     [[maybe_unused]] f32x4 hy[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      if (kb == 1 && !two) break;       // <= 32 unique history rows: one 32-row block
-      if (LOSS && kb == 1) {
-        x2_tr_reads<1>(hb, trH, trL, rh[1], rl[1]);
-        x2_tr_wait<0>(rh[1], rl[1]);
-      }
+      if (kb == 1 && nkb < 2) break;    // <= 32 unique history rows: one 32-row block
       u32x4 eH[2], eL[2];
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl) {
-        eH[ctl] = u32x4{rh[kb][ctl][0].x, rh[kb][ctl][0].y, rh[kb][ctl][1].x, rh[kb][ctl][1].y};
-        eL[ctl] = u32x4{rl[kb][ctl][0].x, rl[kb][ctl][0].y, rl[kb][ctl][1].x, rl[kb][ctl][1].y};
+        const uint2 h0 = lds_tr(part + trH[ctl][0] + 8192 * kb), h1 = lds_tr(part + trH[ctl][1] + 8192 * kb);
+        const uint2 l0 = lds_tr(part + trL[ctl][0] + 8192 * kb), l1 = lds_tr(part + trL[ctl][1] + 8192 * kb);
+        eH[ctl] = u32x4{h0.x, h0.y, h1.x, h1.y};
+        eL[ctl] = u32x4{l0.x, l0.y, l1.x, l1.y};
       }
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl) hx[ctl] = mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
@@ -820,7 +766,20 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
             make_float4(hx[ctl][0] * mui_scale, hx[ctl][1] * mui_scale, hx[ctl][2] * mui_scale, hx[ctl][3] * mui_scale);
     }
     if constexpr (NT > 0) {
-      if constexpr (!kEarly) cand_reads();
+      // candidate operands: each tile's rows from its own base register (opaque to hipcc), so the
+      // reads of tiles q and q + 1 are not paired into a ds_read2st64_b64, whose 16-lane groups bank
+      // by dword mod 32 — a 2-way conflict on these 16-row reads (MI355X_MICROARCH.md §LDS) —
+      // while ds_read_b64 banks mod 64 over 32 lanes: none
+      const char* cpart = slot + 2 * kPart;
+      uint2 cH_[NT][2], cL_[NT][2];
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+#pragma unroll
+        for (int ctl = 0; ctl < 2; ++ctl) {
+          cH_[q][ctl] = lds_u64(cpart + cfH[ctl] + kCTile * q);
+          cL_[q][ctl] = lds_u64(cpart + cfL[ctl] + kCTile * q);
+        }
+      }
       float x[8];
       // mui path: κ·mui·2^-14 (< 2^14); X path: the GELU's input (A·proj)_k = acc / κ, then
       // gelu·κ·2^-14 (|gelu(y)| <= |y|)
@@ -838,7 +797,6 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
       u32x4 bH, bL;
       split8h(x, bH, bL);
-      x2_lds_wait<NT>(cH_, cL_);
       X2_STAMP(5);
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
@@ -849,17 +807,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       X2_STAMP(6);
     }
   };
-  auto compute = [&](int ci, int cc, int mode, int ntile, auto&& dma) {
+  auto compute = [&](int ci, int cc, int mode, int ntile) {
     using std::integral_constant;
-    if (!(mode & 1)) {
-      dma();
-      return;
-    }
-    if (!(mode & 2)) compute_t(ci, cc, mode, integral_constant<int, 0>{}, dma);
-    else if (ntile >= 4) compute_t(ci, cc, mode, integral_constant<int, 4>{}, dma);
-    else if (ntile == 3) compute_t(ci, cc, mode, integral_constant<int, 3>{}, dma);
-    else if (ntile == 2) compute_t(ci, cc, mode, integral_constant<int, 2>{}, dma);
-    else compute_t(ci, cc, mode, integral_constant<int, 1>{}, dma);
+    if (!(mode & 1)) return;
+    if (!(mode & 2)) compute_t(ci, cc, mode, integral_constant<int, 0>{});
+    else if (ntile >= 4) compute_t(ci, cc, mode, integral_constant<int, 4>{});
+    else if (ntile == 3) compute_t(ci, cc, mode, integral_constant<int, 3>{});
+    else if (ntile == 2) compute_t(ci, cc, mode, integral_constant<int, 2>{});
+    else compute_t(ci, cc, mode, integral_constant<int, 1>{});
   };
 
   // static priority for the X waves 4-7 (the GELU chain)
@@ -911,14 +866,15 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         } else if (cc == 1 && cp == 0) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
         }
-        compute(ci, cc, mode, ntile, [&]() {
-          if (cc + 1 < nchunk) {
-            dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
-          } else {
-            item_offsets(ni, np, nH, nC, nLv);
-            dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
-          }
-        });
+        X2_STAMP(2);
+        if (cc + 1 < nchunk) {
+          dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
+        } else {
+          item_offsets(ni, np, nH, nC, nLv);
+          dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
+        }
+        X2_STAMP(3);
+        compute(ci, cc, mode, ntile);
       }
       if (WITH_CAND && wave >= 4) {
         // this pass's S7 (after the next barrier) needs its candidates' row units: one per lane

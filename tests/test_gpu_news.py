@@ -171,7 +171,7 @@ def _heavy_tailed(seed, B=240, L=50, d=768, n_news=4000, C=40):
     the rest never do."""
     g = torch.Generator().manual_seed(seed)
     t = torch.randn((n_news, d), generator=g) / d ** 0.5
-    t[:, [5, 77, 400]] *= 100.0
+    t[:, [5, 77, d // 2 + 16]] *= 100.0
     t[1] *= 1e4
     t[2] *= 1e5
     hid = torch.randint(3, n_news, (B, L), generator=g)

@@ -1,7 +1,8 @@
 """A/B of the news scoring kernels across commits (news.hip of each commit built alone).
 
     python tools/bisect_news.py --build C1 C2 ...            # CPU: tools/bisect/libnews_<C>.so
-    python tools/bisect_news.py [--dtype fp32|bf16] [--B N] C1 C2 ...   # GPU: interleaved timing
+    python tools/bisect_news.py --build wt:NAME[:FLAG,FLAG]  # the working tree's news.hip with -D flags
+    python tools/bisect_news.py [--dtype fp32|bf16] [--B N] [--d 256 --n-news 65238] C1 C2 ...   # GPU
 
 Every version runs the same inputs (config 3: L=50, K=32, d=768, C=40, 104k-row table) through its
 own precompute and scoring entry points in one process, reps interleaved; prints the median ms per
@@ -22,6 +23,16 @@ def build(commits):
     sys.path.insert(0, ROOT)
     from miner_amd.build import hipcc
     for c in commits:
+        if c.startswith("wt:"):
+            parts = c.split(":")
+            name, flags = parts[1], (["-D" + f for f in parts[2].split(",")] if len(parts) > 2 and parts[2] else [])
+            os.makedirs(OUT, exist_ok=True)
+            lib = os.path.join(OUT, f"libnews_{name}.so")
+            subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-pass-failed",
+                            *flags, "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "miner_amd", "csrc", "news.hip"),
+                            "-o", lib], check=True)
+            print("built", lib, flush=True)
+            continue
         src = os.path.join("/tmp", "bisect_news", c)
         for sub in ("miner_amd/csrc", "include"):
             os.makedirs(os.path.join(src, sub), exist_ok=True)
@@ -40,13 +51,13 @@ def build(commits):
         print("built", lib, flush=True)
 
 
-def run(commits, dtype, B, reps):
+def run(commits, dtype, B, reps, d=768, n_news=104000):
     import torch
     sys.path.insert(0, ROOT)
     from miner_amd import ops, synthetic
     P, I = ctypes.c_void_p, ctypes.c_int
     dev = "cuda:0"
-    n_news, L, C, d, K, Dc = 104000, 50, 40, 768, 32, 200
+    L, C, K, Dc = 50, 40, 32, 200
     dt = torch.float32 if dtype == "fp32" else torch.bfloat16
     code = 0 if dtype == "fp32" else 1
     g = torch.Generator(device=dev).manual_seed(36)
@@ -62,7 +73,7 @@ def run(commits, dtype, B, reps):
     st = torch.cuda.current_stream().cuda_stream
     runs = {}
     for c in commits:
-        h = ctypes.CDLL(os.path.join(OUT, f"libnews_{c}.so"))
+        h = ctypes.CDLL(os.path.join(OUT, f"libnews_{c.split(':')[1] if c.startswith('wt:') else c}.so"))
         h.miner_news_precompute.argtypes = [P, I, P, I, P, I, I, I, P, P]
         h.miner_score_news.argtypes = [P, I, I, P, P, P, I, P, P, P, P, P, I, I, I, I, I, P, P]
         logits = torch.empty((n_news, K), device=dev)
@@ -104,9 +115,11 @@ if __name__ == "__main__":
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--B", type=int, default=1000000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--d", type=int, default=768)
+    ap.add_argument("--n-news", type=int, default=104000)
     ap.add_argument("commits", nargs="+")
     a = ap.parse_args()
     if a.build:
         build(a.commits)
     else:
-        run(a.commits, a.dtype, a.B, a.reps)
+        run(a.commits, a.dtype, a.B, a.reps, a.d, a.n_news)

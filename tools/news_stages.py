@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 STAGES = ["vm_wait (row DMAs)", "barrier", "item start / softmax / aux", "DMA issue",
           "history product", "gelu + split", "candidate product", "pass end + loop"]
-STAGESX2 = ["vm_wait (row DMAs)", "barrier", "item start / S7 / softmax / aux", "DMA issue",
+STAGESX2 = ["vm_wait (row DMAs)", "barrier", "item/S7/softmax/aux+LDS rd", "DMA issue",
             "history product", "scale + gelu + split", "candidate product", "pass end + loop"]
 STAGES16 = ["slot wait + barrier", "item start rest / aux", "softmax phases", "DMA issue", "history product",
             "gelu + frag", "cand product + pass end", "S7"]
@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--batch", type=int, default=32768)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "x2"])
+    ap.add_argument("--d", type=int, default=768, help="embedding dim (256 with --n-news 65238: config 2)")
+    ap.add_argument("--n-news", type=int, default=104000)
     args = ap.parse_args()
     import stage_profile
     if args.build:
@@ -43,7 +45,7 @@ def main():
     fn.argtypes = [ctypes.c_void_p]
     fn.restype = ctypes.c_int
     dev = "cuda:0"
-    B, n_news, L, C, d, K, Dc = args.batch, 104000, 50, 40, 768, 32, 200
+    B, n_news, L, C, d, K, Dc = args.batch, args.n_news, 50, 40, args.d, 32, 200
     g = torch.Generator(device=dev).manual_seed(36)
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     table = (torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5).to(dt)
@@ -69,7 +71,7 @@ def main():
     n = out[64]
     kind = "fp32 news_score_x2 (fp16 pairs)" if x2 else "bf16 news_score" if args.dtype == "bf16" else \
         f"fp32 news_score32 ({'bf16x6' if os.environ.get('MINER_NEWS_F32X6') else 'fp32 MFMA'})"
-    print(f"{kind} B={B}: "
+    print(f"{kind} B={B} d={d}: "
           f"{ms:.3f} ms/launch ({ms / B * 131072:.2f} ms per 131k), cycles per impression per workgroup:")
     print(f"  {'stage':28s}" + "".join(f"  wave{w}" for w in range(8)))
     names = STAGES16 if args.dtype == "bf16" else STAGES

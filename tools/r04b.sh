@@ -1,8 +1,13 @@
+# Round-4 GPU session (tools/r04b.sh TAG): parity tests of the news path, x2 stage profile, x2 A/B of
+# kernel variants built in tools/bisect/ (X2AB names).
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 O=gpurun_out/${1:-r04b}; mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_news.py tests/test_gpu_eval_loop.py tests/test_gpu_fullsize.py -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
 tail -3 $O/tests.log; grep -E "^FAILED|Error" $O/tests.log | head -20
 [ $rc -ge 124 ] && exit $rc
-shift || true
-bash tools/r04_check.sh ${O#gpurun_out/} 0 1 "$@"
+timeout -k 10 300 python3 tools/news_stages.py --dtype x2 --batch 131072 > "$O/x2_stages.txt" 2>&1 || { tail -20 "$O/x2_stages.txt"; exit 1; }
+cat "$O/x2_stages.txt"
+AB="${X2AB:-base cexp cur}"
+timeout -k 10 400 python3 tools/x2_ab.py $AB > "$O/x2_ab.txt" 2>&1 || { tail -20 "$O/x2_ab.txt"; exit 1; }
+cat "$O/x2_ab.txt"
