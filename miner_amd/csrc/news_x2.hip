@@ -57,6 +57,12 @@
 
 namespace {
 
+#ifndef X2_ABL
+#define X2_ABL 0       // timing ablations only (wrong scores): 2 no row DMAs, 4 no products, 8 no GELU, 16 no candidate MFMAs, 32 no history MFMAs
+#endif
+#ifndef X2_DMA_EARLY
+#define X2_DMA_EARLY 1 // the next chunk's row DMAs issued right after the barrier, before a pass start's S7 / softmax / aux work
+#endif
 constexpr int kNB = 2;                                 // row-DMA blocks per wave per part
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
@@ -497,7 +503,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     lv = __builtin_amdgcn_readfirstlane(lv);
   };
   auto dma_chunk = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int cc, int slot) {
-    if (lv == 0) return;
+    if (lv == 0 || (X2_ABL & 2)) return;
     const char* bE = tabB + cc * kRB;
     const char* bP = prjB + cc * kRB;
 #pragma unroll
@@ -732,7 +738,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         eL[ctl] = u32x4{l0.x, l0.y, l1.x, l1.y};
       }
 #pragma unroll
-      for (int ctl = 0; ctl < 2; ++ctl) hx[ctl] = mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
+      for (int ctl = 0; ctl < 2; ++ctl)
+        hx[ctl] = (X2_ABL & 32) ? f32x4{__uint_as_float(eH[ctl][0] ^ aH[kb][0]), __uint_as_float(eL[ctl][1] ^ aL[kb][1]), 0.f, 0.f}
+                                : mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
       if (LOSS && (mode & 8)) {
 #pragma unroll
         for (int ctl = 0; ctl < 2; ++ctl) hy[ctl] = mfma_x2(hy[ctl], eH[ctl], eL[ctl], aH1[kb], aL1[kb]);
@@ -790,7 +798,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         x[4 + e] = hx[1][e] * op_scale;
       }
       if (WEIGHTED && P == 1) {
-        gelu_as_pairs(x, 8);
+        if (!(X2_ABL & 8)) gelu_as_pairs(x, 8);
         const float sPj = kap * (1.0f / kSA);
 #pragma unroll
         for (int e = 0; e < 8; ++e) x[e] *= sPj;
@@ -802,14 +810,15 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       for (int q = 0; q < NT; ++q) {
         const u32x4 ah = u32x4{cH_[q][0].x, cH_[q][0].y, cH_[q][1].x, cH_[q][1].y};
         const u32x4 al = u32x4{cL_[q][0].x, cL_[q][0].y, cL_[q][1].x, cL_[q][1].y};
-        acc[q] = mfma_x2(acc[q], ah, al, bH, bL);
+        if (X2_ABL & 16) acc[q][0] += __uint_as_float(ah[0] ^ al[1] ^ bH[q] ^ bL[q]);
+        else acc[q] = mfma_x2(acc[q], ah, al, bH, bL);
       }
       X2_STAMP(6);
     }
   };
   auto compute = [&](int ci, int cc, int mode, int ntile) {
     using std::integral_constant;
-    if (!(mode & 1)) return;
+    if (!(mode & 1) || (X2_ABL & 4)) return;
     if (!(mode & 2)) compute_t(ci, cc, mode, integral_constant<int, 0>{});
     else if (ntile >= 4) compute_t(ci, cc, mode, integral_constant<int, 4>{});
     else if (ntile == 3) compute_t(ci, cc, mode, integral_constant<int, 3>{});
@@ -840,6 +849,15 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         X2_STAMP(0);
         raw_barrier();                 // then for every wave; the other slot is free
         X2_STAMP(1);
+        auto issue_next = [&]() {
+          if (cc + 1 < nchunk) {
+            dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
+          } else {
+            item_offsets(ni, np, nH, nC, nLv);
+            dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
+          }
+        };
+        if (X2_DMA_EARLY) issue_next();
         if (cc == 0) {
           did_s7 = (WITH_CAND && pend_off >= 0) || d_pending;
           if (WITH_CAND && pend_off >= 0) s7();
@@ -867,12 +885,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
         }
         X2_STAMP(2);
-        if (cc + 1 < nchunk) {
-          dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
-        } else {
-          item_offsets(ni, np, nH, nC, nLv);
-          dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
-        }
+        if (!X2_DMA_EARLY) issue_next();
         X2_STAMP(3);
         compute(ci, cc, mode, ntile);
       }
