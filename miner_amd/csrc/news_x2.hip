@@ -60,6 +60,9 @@ namespace {
 #ifndef X2_ABL
 #define X2_ABL 0       // timing ablations only (wrong scores): 2 no row DMAs, 4 no products, 8 no GELU, 16 no candidate MFMAs, 32 no history MFMAs
 #endif
+#ifndef X2_SOFT_HALF
+#define X2_SOFT_HALF 1 // <= 32 history groups: the softmax over the first 32 only (the second block's A unused)
+#endif
 #ifndef X2_DMA_EARLY
 #define X2_DMA_EARLY 1 // the next chunk's row DMAs issued right after the barrier, before a pass start's S7 / softmax / aux work
 #endif
@@ -549,7 +552,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // softmax over the history groups (model.py:176-181) of this wave's 16 interests, in registers:
   // lane (g, i) takes 16 groups, the 4 lane rows combined by permlanes
   // path pth (0: E rows, 1: proj rows) picks the units; kap = κ_k of this lane's interest
-  auto softmax_inwave = [&](int i, int ktile, int pth, u32x4* dH, u32x4* dL, float& kap) {
+  auto softmax_inwave = [&](int i, int ktile, int pth, u32x4* dH, u32x4* dL, float& kap, auto nss_c) {
+    constexpr int NSS = decltype(nss_c)::value;   // groups per lane: 16 (64 groups) or 8 (the first 32)
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const int k = 16 * ktile + j;
@@ -557,10 +561,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const float* pr = prep_blk(smem, i);
     const int* pc = reinterpret_cast<const int*>(pr);
     const unsigned sh = pth ? 16u : 8u;
-    float v[16], wm[16], un[16];
+    float v[NSS], wm[NSS], un[NSS];
     float mx = -INFINITY;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < NSS; ++s) {
       const int u = 32 * (s >> 3) + 16 * ((s >> 2) & 1) + 4 * g + (s & 3);
       const unsigned code = (unsigned)pc[u];
       wm[s] = (float)(code & 255u);
@@ -572,7 +576,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     mx = x_rows4_max(mx);
     float sum = 0.f, tu = 0.f;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < NSS; ++s) {
       v[s] = x2_exp(v[s] - mx);              // 0 past U (v = -inf there; weight 0)
       const float we = wm[s] * v[s];
       sum += we;
@@ -588,7 +592,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     float inv = kap / sum;
     if (k >= KK) inv = 0.f;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    for (int m = 0; m < NSS / 2; ++m) {
       unsigned h, l;
       split2w(wm[2 * m], v[2 * m], inv * un[2 * m], wm[2 * m + 1], v[2 * m + 1], inv * un[2 * m + 1], h, l);
       dH[m >> 2][m & 3] = h;
@@ -866,10 +870,13 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           pend_d = -1;
           d_pending = false;
           if (cp == 0) {
-            softmax_inwave(ci, kt, P, aH, aL, kap);
+            using std::integral_constant;
+            if (X2_SOFT_HALF && nkb == 1) softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 8>{});
+            else softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 16>{});
             if (LOSS && gram_w && dis_out) {
               float kap1;                // interest tile 1 of the Gram: the Gram's cosines are per-k scale free
-              softmax_inwave(ci, 1, 0, aH1, aL1, kap1);
+              if (X2_SOFT_HALF && nkb == 1) softmax_inwave(ci, 1, 0, aH1, aL1, kap1, integral_constant<int, 8>{});
+              else softmax_inwave(ci, 1, 0, aH1, aL1, kap1, integral_constant<int, 16>{});
             }
             dedupe_prep(ci + 2);       // L1 of ci + 2 landed; its logit rows are DMA'd by group next
             if (nchunk == 1) {
