@@ -834,7 +834,12 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50,
               prefetched = true;
             }
           }
-          if constexpr (kBf16) {
+          // fp32: the last chunk (TAA: every chunk) reduces through the dead mui region with plain
+          // stores like bf16; the earlier chunks of a C > 64 impression still read mui, so they sum
+          // into Lg / Mt with LDS atomics (~190 cycles each: 18 % of the kernel when every chunk did)
+          const bool plain = kBf16 || MODE == kTaa || cc + kCChunk >= Cb;
+          if (!kBf16 && plain) __syncthreads();   // every wave's mui reads (S6 products) done
+          if (plain) {
             s6_reduce_bf16(part, lg, mt, wave, r, h, DBG(3));
           } else {
             if (nm > 0) {
@@ -861,7 +866,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50,
           const int c = cc + cl;
           const bool cval = c < Cb;
           float lgv[4], mtv[4];
-          if constexpr (kBf16) {
+          if (kBf16 || MODE == kTaa || cc + kCChunk >= Cb) {
             s7_load_bf16(part, cl, sub, lgv, mtv);
           } else {
 #pragma unroll
@@ -961,8 +966,8 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   const int pbytes = round16(64 * c.PS * es);
   const int r2a = 32 * c.MS;
   int r2b = bf ? n_ctiles(Dc) * kSPTile * 4 : pbytes + kMaxK * kMaxL * 4;
-  if (bf && parts > r2b) r2b = parts;      // bf16 full: the S6 partial slabs live here too
-  const int r2 = round16(mode == kFull ? (r2a > r2b ? r2a : r2b) : r2a);
+  if (parts > r2b) r2b = parts;            // the S6 partial slabs live here too (after the mui reads)
+  const int r2 = round16(mode == kFull ? (r2a > r2b ? r2a : r2b) : (r2a > parts ? r2a : parts));
   const int aw = mode == kFull ? (bf ? 32 * 72 * 2 : 32 * 68 * 4) : 0;
   int off = 0;
   if (bf) {
@@ -985,6 +990,7 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   c.offP = c.offMui;                       // P lives in the mui region until S4 overwrites it
   c.offS = bf ? c.offMui : c.offMui + pbytes;   // S too (bf16: the per-wave S partials of S1)
   if (bf && mode == kFull) c.offPart = c.offMui;   // full: after S6 products mui is dead
+  if (!bf) c.offPart = c.offMui;                   // fp32: the last chunk's partials (after its products)
   c.offAw = round16(c.offMui + r2);
   c.total = c.offAw + aw;
   if (!bf && mode == kFull) {   // fp32 gather mode: the impression's history ids
