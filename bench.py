@@ -656,8 +656,15 @@ def dense_kernel_line(dev, B=32768, steps=10):
     from miner_amd import ops, synthetic
     W1, Q, W2 = synthetic.init_weights(36, D, DC, K, device=dev)
     out = {}
+    prev = os.environ.get("MINER_DENSE_FP32")
     for name, dt, peak, n in (("bf16", torch.bfloat16, PEAK_BF16_TFLOPS, B), ("fp32", torch.float32, PEAK_F32_TFLOPS,
-                                                                               B // 4)):
+                                                                               B // 4),
+                              ("fp32_mfma_exact", torch.float32, PEAK_F32_TFLOPS, B // 4)):
+        # fp32: S1 / S5 as bf16x6 (the default); fp32_mfma_exact: every product on the fp32 MFMA
+        if name == "fp32_mfma_exact":
+            os.environ["MINER_DENSE_FP32"] = "mfma32"
+        elif prev is None:
+            os.environ.pop("MINER_DENSE_FP32", None)
         imp = synthetic.impressions(36, 0, n, L=L, d=D, C=C, device=dev, dtype=dt)
         pw = ops.pack_weights(W1, Q, W2, dtype=dt)
         for _ in range(3):
@@ -675,13 +682,24 @@ def dense_kernel_line(dev, B=32768, steps=10):
         tf = fl / (ms / 1e3) / 1e12
         by = bytes_per_impression(L, D, C, 2 if name == "bf16" else 4) * n
         del imp
-        out[name] = {"kernel": f"miner_fused<{name},full>", "value": round(n * C / (ms / 1e3), 1), "unit": "pairs/s",
+        kname = {"bf16": "miner_fused<bf16,full>", "fp32": "miner_fused<fp32,full,bf16x6 S1/S5>",
+                 "fp32_mfma_exact": "miner_fused<fp32,full>"}[name]
+        out[name] = {"kernel": kname, "value": round(n * C / (ms / 1e3), 1), "unit": "pairs/s",
                      "ms_per_launch": round(ms, 4), "impressions": n,
                      "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
                                   "frac": round(tf / peak, 4), "flops_per_launch": fl,
                                   "hbm_frac": round(by / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}}
+    if prev is None:
+        os.environ.pop("MINER_DENSE_FP32", None)
+    else:
+        os.environ["MINER_DENSE_FP32"] = prev
     out["note"] = ("Miner.score / Miner.forward's drop-in module path on dense [B, L, d] / [B, C, d] rows: every "
-                   "impression re-reads W1 and W2 (the news-id path precomputes them per news row instead)")
+                   "impression re-reads W1 and W2 (the news-id path precomputes them per news row instead). fp32: "
+                   "S1 (W1·Eᵀ) and S5 (W2·muiᵀ) as bf16x6 (each fp32 operand cut exactly into three bf16 terms, the "
+                   "six leading partial products on the bf16 MFMA; error vs float64 within 1.5x the fp32 MFMA's, "
+                   "tests/test_gpu_parity.py::test_x6_error_vs_fp32_mfma), S2 / S4 / S6 on the fp32 MFMA; its "
+                   "frac is algorithmic FLOPs over the fp32 peak. fp32_mfma_exact: every product on the fp32 MFMA "
+                   "(MINER_DENSE_FP32=mfma32)")
     return out
 
 

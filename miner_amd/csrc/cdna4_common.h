@@ -231,6 +231,41 @@ __device__ __forceinline__ f32x4 mma_x6(f32x4 c, const Split8& a, const Split8& 
   return mfma16_bf16(a.hi, b.hi, c);
 }
 
+// The same on 32x32 slab fragments (miner_fused<fp32> with X6): a Frag<float> (16 contraction
+// elements per lane) cut into three bf16 terms, the six partial products smallest first —
+// 12 v_mfma_f32_32x32x16_bf16 (384 cycles) for the 1024 cycles of the 16 v_mfma_f32_32x32x2_f32
+// of one slab product.
+// One 16-element step at a time (8 contraction elements per lane), so only 2 x 3 bf16 operand
+// registers quads are live beside the fp32 fragments.
+__device__ __forceinline__ void split8_step(const Frag<float>& f, int st, u32x4& h, u32x4& m, u32x4& l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {               // elements 8st + 2i, 8st + 2i + 1 -> dword i
+    const int e = 8 * st + 2 * i;
+    unsigned hh, mm, ll;
+    split3_pair(__uint_as_float(f.q[e >> 2][e & 3]), __uint_as_float(f.q[(e + 1) >> 2][(e + 1) & 3]), hh, mm, ll);
+    h[i] = hh;
+    m[i] = mm;
+    l[i] = ll;
+  }
+}
+__device__ __forceinline__ f32x16 mfma32_bf16(const u32x4& a, const u32x4& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ void mma_slab_x6(f32x16& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    u32x4 ah, am, al, bh, bm, bl;
+    split8_step(a, st, ah, am, al);
+    split8_step(b, st, bh, bm, bl);
+    acc = mfma32_bf16(al, bh, acc);            // smallest terms first
+    acc = mfma32_bf16(ah, bl, acc);
+    acc = mfma32_bf16(am, bm, acc);
+    acc = mfma32_bf16(am, bh, acc);
+    acc = mfma32_bf16(ah, bm, acc);
+    acc = mfma32_bf16(ah, bh, acc);
+  }
+}
+
 // The fp32 kernels' GELU at fewer VALU: Abramowitz & Stegun 7.1.26, erf(z) = 1 - t·P5(t)·e^{-z²},
 // t = 1/(1 + 0.3275911 z), |Δerf| <= 1.5e-7 for every z >= 0, so |Δgelu| <= 0.75e-7·|x| plus the
 // fp32 rounding: <= 2.2e-7·max(1, |x|) against float64 (tools/gelu_error.py), the accuracy class of

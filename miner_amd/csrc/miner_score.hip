@@ -42,6 +42,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 #include <math.h>
 
 #include "../../include/miner_score.h"
@@ -196,13 +197,24 @@ __device__ unsigned long long g_stage_imps;
 #define DBG(bit) 0
 #endif
 
+// slab product: fp32 MFMA, or (X6, the fp32 kernel's default) the six bf16 partial products of
+// split16 operands — see cdna4_common.h (bf16x6)
+#ifndef MINER_X6_STAGES
+#define MINER_X6_STAGES 5   // bf16x6 stages of the fp32 kernel: 1 S1, 2 S4, 4 S5 (S4 as bf16x6 spills 12-21 VGPRs: off)
+#endif
+template <class T, bool X6>
+__device__ __forceinline__ void mma_f(f32x16& acc, const Frag<T>& a, const Frag<T>& b) {
+  if constexpr (X6 && sizeof(T) == 4) mma_slab_x6(acc, a, b);
+  else mma_slab<T>(acc, a, b);
+}
+
 // ---------------------------------------------------------------------------------------------
 // S5 body, specialised on NM = number of d-tiles the wave owns (tiles wave + 8m)
 // ---------------------------------------------------------------------------------------------
 // X_m = gelu(W2[tile m] · muiᵀ) over the whole contraction d; packed W2 slabs stream from L2
 // through a PF-deep register ring (unconditional loads, clamped at the end), muiᵀ fragments come
 // from LDS.  The result stays in registers as slab fragments of the S6 contraction.
-template <class T, int PF, int NM>
+template <class T, int PF, int NM, bool X6>
 __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restrict__ W2p, const T* muiL,
                                         int msE, int d, int wave, int lane) {
   const int ns = d >> 5;
@@ -227,7 +239,7 @@ __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restric
       Frag<T> bm;
       frag_load(bm, muiL + r * msE + (j + s) * 32 + 16 * h);
 #pragma unroll
-      for (int m = 0; m < NM; ++m) mma_slab<T>(acc[m], ring[s][m], bm);
+      for (int m = 0; m < NM; ++m) mma_f<T, X6 && (MINER_X6_STAGES & 4)>(acc[m], ring[s][m], bm);
 #pragma unroll
       for (int m = 0; m < NM; ++m) frag_load_tile(ring[s][m], w2t[m] + min(j + s + PF, ns - 1) * 1024, lane);
       __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
@@ -239,7 +251,7 @@ __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restric
       Frag<T> bm;
       frag_load(bm, muiL + r * msE + (j + s) * 32 + 16 * h);
 #pragma unroll
-      for (int m = 0; m < NM; ++m) mma_slab<T>(acc[m], ring[s][m], bm);
+      for (int m = 0; m < NM; ++m) mma_f<T, X6 && (MINER_X6_STAGES & 4)>(acc[m], ring[s][m], bm);
     }
   }
 #pragma unroll
@@ -408,8 +420,10 @@ __device__ __forceinline__ float s7_score(const float (&lgv)[4], const float (&m
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
 // ---------------------------------------------------------------------------------------------
-template <class T, int MODE, int NS, bool GATHER, int SHP = 0>   // SHP 1: the MIND model shape compile-time
-__global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50, Dc = 200, K = 32)
+// SHP 1: the MIND model shape compile-time (L = 50, Dc = 200, K = 32); X6 (fp32 only): S1 and
+// S5 on the bf16 matrix cores as bf16x6 (S4 stays on the fp32 MFMA) (the fp32-MFMA form stays selectable: MINER_DENSE_FP32=mfma32)
+template <class T, int MODE, int NS, bool GATHER, int SHP = 0, bool X6 = false>
+__global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kBf16 = sizeof(T) == 2;
   // news-table gather mode (compile-time, so the dense instantiations carry no gather code)
@@ -554,8 +568,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50,
                 Frag<T> b0, b1;
                 frag_load(b0, erow(l0) + kk + 16 * h);
                 frag_load(b1, erow(l1) + kk + 16 * h);
-                mma_slab<T>(acc0, ring[s], b0);
-                mma_slab<T>(acc1, ring[s], b1);
+                mma_f<T, X6 && (MINER_X6_STAGES & 1)>(acc0, ring[s], b0);
+                mma_f<T, X6 && (MINER_X6_STAGES & 1)>(acc1, ring[s], b1);
                 frag_load_tile(ring[s], w1t + min(j + s + PF1, ns - 1) * 1024, lane);
                 __builtin_amdgcn_sched_barrier(0);
               }
@@ -567,8 +581,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50,
                 Frag<T> b0, b1;
                 frag_load(b0, erow(l0) + kk + 16 * h);
                 frag_load(b1, erow(l1) + kk + 16 * h);
-                mma_slab<T>(acc0, ring[s], b0);
-                mma_slab<T>(acc1, ring[s], b1);
+                mma_f<T, X6 && (MINER_X6_STAGES & 1)>(acc0, ring[s], b0);
+                mma_f<T, X6 && (MINER_X6_STAGES & 1)>(acc1, ring[s], b1);
               }
             }
           }
@@ -736,7 +750,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50,
                 }
               }
               if constexpr (kBf16) mma_slab<T>(acc, bf, ls == 0 ? af0 : af1);   // muiᵀ = Eᵀ·Aᵀ
-              else mma_slab<T>(acc, ls == 0 ? af0 : af1, bf);
+              else mma_f<T, X6 && (MINER_X6_STAGES & 2)>(acc, ls == 0 ? af0 : af1, bf);
             }
           }
           if constexpr (kBf16) {
@@ -795,9 +809,9 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {  // (L = 50,
         FRESH_LANE_IDS();
         const int nm = (ns - wave + kWaves - 1) / kWaves;
         if (weighted) {
-          if (nm == 3) s5_gelu<T, PF, 3>(xf, W2p, muiL, msE, d, wave, lane);
-          else if (nm == 2) s5_gelu<T, PF, 2>(xf, W2p, muiL, msE, d, wave, lane);
-          else if (nm == 1) s5_gelu<T, PF, 1>(xf, W2p, muiL, msE, d, wave, lane);
+          if (nm == 3) s5_gelu<T, PF, 3, X6>(xf, W2p, muiL, msE, d, wave, lane);
+          else if (nm == 2) s5_gelu<T, PF, 2, X6>(xf, W2p, muiL, msE, d, wave, lane);
+          else if (nm == 1) s5_gelu<T, PF, 1, X6>(xf, W2p, muiL, msE, d, wave, lane);
         }
       }
       Frag<T> am[kMaxJ];   // bf16 full: the wave's mui fragments, held across the candidate chunks
@@ -1024,9 +1038,9 @@ int num_cus() {
 
 inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <class T, int MODE, int NS, bool GATHER = false, int SHP = 0>
+template <class T, int MODE, int NS, bool GATHER = false, int SHP = 0, bool X6 = false>
 int launch(void* stream, const Params& prm, int lds) {
-  auto kern = miner_fused<T, MODE, NS, GATHER, SHP>;
+  auto kern = miner_fused<T, MODE, NS, GATHER, SHP, X6>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   const int per_cu = kLdsMax / lds > 0 ? (kLdsMax / lds > 2 ? 2 : kLdsMax / lds) : 1;
@@ -1066,8 +1080,14 @@ int run(void* stream, int dtype, int mode, Params prm) {
         return gather ? launch<__bf16, kFull, 0, true>(stream, prm, c.total) : launch<__bf16, kFull, 0>(stream, prm, c.total);
     }
   }
-  if (mode == kTaa) return launch<float, kTaa, 0>(stream, prm, c.total);
-  return gather ? launch<float, kFull, 0, true>(stream, prm, c.total) : launch<float, kFull, 0>(stream, prm, c.total);
+  // fp32: bf16x6 products by default, the exact fp32-MFMA form on MINER_DENSE_FP32=mfma32
+  const char* f32mode = getenv("MINER_DENSE_FP32");
+  if (f32mode && strcmp(f32mode, "mfma32") == 0) {
+    if (mode == kTaa) return launch<float, kTaa, 0>(stream, prm, c.total);
+    return gather ? launch<float, kFull, 0, true>(stream, prm, c.total) : launch<float, kFull, 0>(stream, prm, c.total);
+  }
+  if (mode == kTaa) return launch<float, kTaa, 0, false, 0, true>(stream, prm, c.total);
+  return gather ? launch<float, kFull, 0, true, 0, true>(stream, prm, c.total) : launch<float, kFull, 0, false, 0, true>(stream, prm, c.total);
 }
 
 size_t packed_bytes(int dtype, int d, int Dc) {

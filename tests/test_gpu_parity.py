@@ -38,8 +38,15 @@ def _inputs(g, dtype):
             _dev(g["Q"], dtype), W2, bias)
 
 
+@pytest.mark.parametrize("form", ["x6", "mfma32"])
 @pytest.mark.parametrize("name", golden_names())
-def test_fp32_matches_reference(name):
+def test_fp32_matches_reference(name, form, monkeypatch):
+    """fp32 mode in both forms of the dense kernel: bf16x6 products on the bf16 matrix cores (the
+    default) and the exact fp32-MFMA fma chains (MINER_DENSE_FP32=mfma32)."""
+    if form == "mfma32":
+        monkeypatch.setenv("MINER_DENSE_FP32", "mfma32")
+    else:
+        monkeypatch.delenv("MINER_DENSE_FP32", raising=False)
     g = load_golden(name)
     E, M, Cd, W1, Q, W2, bias = _inputs(g, torch.float32)
     scores, mui = _ops().score(E, M, Cd, W1, Q, W2, score_type=g["score_type"], his_bias=bias, return_user=True)
@@ -179,3 +186,38 @@ def test_cpu_tensors_fail_loudly():
     with pytest.raises(RuntimeError):
         _ops().score(E, torch.ones((2, 4), dtype=torch.bool), torch.zeros((2, 3, 64)),
                      torch.zeros((8, 64)), torch.zeros((4, 8)), torch.zeros((64, 64)))
+
+
+@pytest.mark.parametrize("scale,score_type", [(1.0, "weighted"), (1.0, "max"), (1e-3, "weighted"), (300.0, "max")])
+def test_x6_error_vs_fp32_mfma(scale, score_type, monkeypatch):
+    """The dense fp32 kernel's bf16x6 products are as accurate as the fp32 MFMA: against float64
+    (oracle.score_f64) the worst error per unit of the parity bar (|x - ref| / (|ref| + rms)) and the
+    rms error stay within 1.5x those of the exact fp32 fma chains (bf16 keeps fp32's exponent range,
+    so the row scale does not matter; 300 and 1e-3 check that — at 300 the 'weighted' softmax over K
+    is one-hot and ill-conditioned in any fp32 form, so that scale is checked on 'max')."""
+    g = torch.Generator().manual_seed(61)
+    B, L, C, d, Dc, K = 96, 50, 40, 768, 200, 32
+    E = torch.randn((B, L, d), generator=g) / d ** 0.5 * scale
+    cand = torch.randn((B, C, d), generator=g) / d ** 0.5 * scale
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    mask = torch.arange(L)[None, :] >= (L - lens)[:, None]
+    W1 = torch.randn((Dc, d), generator=g) * (2.0 / (Dc + d)) ** 0.5
+    Q = torch.randn((K, Dc), generator=g) * (2.0 / (K + Dc)) ** 0.5
+    W2 = torch.randn((d, d), generator=g) * (1.0 / d) ** 0.5
+    _, ref = orc.score_f64(E.numpy(), mask.numpy(), cand.numpy(), W1.numpy(), Q.numpy(), W2.numpy(), score_type)
+    ref = torch.from_numpy(ref)
+    rms = float(ref.pow(2).mean().sqrt())
+    errs = {}
+    for form in ("x6", "mfma32"):
+        if form == "mfma32":
+            monkeypatch.setenv("MINER_DENSE_FP32", "mfma32")
+        else:
+            monkeypatch.delenv("MINER_DENSE_FP32", raising=False)
+        s = _ops().score(E.to(DEV), mask.to(DEV), cand.to(DEV), W1.to(DEV), Q.to(DEV), W2.to(DEV), score_type=score_type)
+        torch.cuda.synchronize()
+        e = (s.double().cpu() - ref).abs()
+        errs[form] = (float((e / (ref.abs() + rms)).max()), float(e.pow(2).mean().sqrt()))
+        ok, worst = orc.parity_ok(s.cpu().numpy(), ref.numpy())
+        assert ok, f"{form} at scale {scale} ({score_type}): off by {worst:.2f}x the tolerance"
+    assert errs["x6"][0] <= 1.5 * errs["mfma32"][0] + 1e-7, errs
+    assert errs["x6"][1] <= 1.5 * errs["mfma32"][1] + 1e-8 * rms, errs
