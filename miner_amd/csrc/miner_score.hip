@@ -200,7 +200,7 @@ __device__ unsigned long long g_stage_imps;
 // slab product: fp32 MFMA, or (X6, the fp32 kernel's default) the six bf16 partial products of
 // split16 operands — see cdna4_common.h (bf16x6)
 #ifndef MINER_X6_STAGES
-#define MINER_X6_STAGES 5   // bf16x6 stages of the fp32 kernel: 1 S1, 2 S4, 4 S5 (S4 as bf16x6 spills 12-21 VGPRs: off)
+#define MINER_X6_STAGES 5   // bf16x6 stages of the fp32 kernel: 1 S1, 2 S4, 4 S5, 8 S6 (S4 spills 12-21 VGPRs, S6 61-74: off)
 #endif
 template <class T, bool X6>
 __device__ __forceinline__ void mma_f(f32x16& acc, const Frag<T>& a, const Frag<T>& b) {
@@ -264,7 +264,7 @@ __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restric
 // S6 partial products over the wave's d-tiles for candidates [cc, cc+64): lg = Xᵀ·Candᵀ and
 // mt = mui·Candᵀ restricted to those tiles.  Candidate rows past the end are clamped to a real
 // row (finite data, never read back by S7).
-template <class T, int NM, bool WEIGHTED, bool FULL>
+template <class T, int NM, bool WEIGHTED, bool FULL, bool X6>
 __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
                                             const Frag<T> (&amr)[kMaxJ], const T* __restrict__ cand,
                                             const char* cimg, int Cb, int cc, int d, int wave, int r, int h,
@@ -302,20 +302,20 @@ __device__ __forceinline__ void s6_products(f32x16 (&lg)[2], f32x16 (&mt)[2], co
     mt[ct] = zero16();
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      if constexpr (WEIGHTED) mma_slab<T>(lg[ct], xf[m], bc[m]);
-      if constexpr (FULL) mma_slab<T>(mt[ct], am[m], bc[m]);
+      if constexpr (WEIGHTED) mma_f<T, X6 && (MINER_X6_STAGES & 8)>(lg[ct], xf[m], bc[m]);
+      if constexpr (FULL) mma_f<T, X6 && (MINER_X6_STAGES & 8)>(mt[ct], am[m], bc[m]);
     }
   }
 }
 
-template <class T, bool WEIGHTED, bool FULL>
+template <class T, bool WEIGHTED, bool FULL, bool X6>
 __device__ __forceinline__ void s6_dispatch(int nm, f32x16 (&lg)[2], f32x16 (&mt)[2], const Frag<T> (&xf)[kMaxJ],
                                             const Frag<T> (&am)[kMaxJ], const T* cand, const char* cimg, int Cb,
                                             int cc, int d, int wave, int r, int h, const T* muiL, int msE,
                                             const int32_t* cids, int n_news) {
-  if (nm == 3) s6_products<T, 3, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
-  else if (nm == 2) s6_products<T, 2, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
-  else if (nm == 1) s6_products<T, 1, WEIGHTED, FULL>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
+  if (nm == 3) s6_products<T, 3, WEIGHTED, FULL, X6>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
+  else if (nm == 2) s6_products<T, 2, WEIGHTED, FULL, X6>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
+  else if (nm == 1) s6_products<T, 1, WEIGHTED, FULL, X6>(lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, n_news);
 }
 
 // one 32x32 accumulator tile -> rows [c][k] of a partial slab (4 x 16-byte stores per lane):
@@ -833,8 +833,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           const int nm = (ns - wave + kWaves - 1) / kWaves;
           f32x16 lg[2], mt[2];
           lg[0] = lg[1] = mt[0] = mt[1] = zero16();
-          if (weighted) s6_dispatch<T, true, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
-          else s6_dispatch<T, false, MODE == kFull>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
+          if (weighted) s6_dispatch<T, true, MODE == kFull, X6>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
+          else s6_dispatch<T, false, MODE == kFull, X6>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
           STAMP_SYNC();
           STAMP(6);
           if constexpr (kDma) {
