@@ -97,6 +97,9 @@ __device__ __forceinline__ u32x4 lds_u32x4(const char* p) { return *reinterpret_
 #ifndef NS_D256_CW128
 #define NS_D256_CW128 0
 #endif
+#ifndef NS_ABL
+#define NS_ABL 0         // timing ablations of news_score (wrong scores): 2 no row DMAs, 4 no products
+#endif
 #ifndef NS_EARLY
 #define NS_EARLY 0       // 1: operand reads issued before the chunk's row DMAs (measured 25 % slower at d = 768)
 #endif
@@ -1153,10 +1156,11 @@ __global__ __launch_bounds__(kThreads) void news_score(NsParams p) {
       }
       return;
     }
-    dma_chunk<T, CW, SKIP, WEIGHTED>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
-                                     sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024, iLv, (w4 + 8 - wave) * 1024);
+    if (!(NS_ABL & 2))
+      dma_chunk<T, CW, SKIP, WEIGHTED>(iH, iC, tabB + ich * CW * sizeof(T), prjB + ich * CW * sizeof(T),
+                                       sbase + ((t + PD) & (NS - 1)) * Cf::SLOT + wave * 1024, iLv, (w4 + 8 - wave) * 1024);
     NS_STAMP(3);
-    if (mode & 1) {
+    if ((mode & 1) && !(NS_ABL & 4)) {
       FRESH_LANE_IDS();
       const char* slot = smem + (t & (NS - 1)) * Cf::SLOT;
       const char* part = slot + P * Cf::PART;
