@@ -30,12 +30,15 @@ def main():
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "x2"])
     ap.add_argument("--d", type=int, default=768, help="embedding dim (256 with --n-news 65238: config 2)")
     ap.add_argument("--n-news", type=int, default=104000)
+    ap.add_argument("--lib", default=None, help="a stamps library built with extra flags (default: the stamps build)")
+    ap.add_argument("--flags", default="", help="--build: extra -D flags, comma separated (with --lib as the output)")
     args = ap.parse_args()
     import stage_profile
     if args.build:
-        stage_profile.build()
+        extra = ["-D" + f for f in args.flags.split(",") if f]
+        stage_profile.build(extra, out=args.lib or stage_profile.STAMP_LIB)
         return
-    os.environ["MINER_HIP_LIB"] = stage_profile.STAMP_LIB
+    os.environ["MINER_HIP_LIB"] = args.lib or stage_profile.STAMP_LIB
     import torch
     from miner_amd import _lib, news, ops, synthetic
     x2 = args.dtype == "x2"
