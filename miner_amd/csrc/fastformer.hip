@@ -172,7 +172,12 @@ constexpr int kSwBytes = kHeads * kMaxL * 4;           // [16 heads][64 rows] fp
 // parity mode has no room for them and reads them from L2
 template <class T> constexpr int kVecLds = sizeof(T) == 2 ? kVecSlots * kH * 4 : 0;
 template <class T> constexpr int kOffVec = 2 * kImg<T> + kRedBytes + kSwBytes + kH * 4;
-template <class T> constexpr int kLdsTotal = kOffVec<T> + kVecLds<T>;
+#ifndef FF_MQK_LDS
+#define FF_MQK_LDS 0   // experiment (bf16): mq / mk in two bf16 LDS images instead of fp32 registers, the
+                       // 29 vector slots read from L2 — the first step toward two impressions per CU
+#endif
+template <class T> constexpr bool kMqkLds = FF_MQK_LDS && sizeof(T) == 2;
+template <class T> constexpr int kLdsTotal = kOffVec<T> + (kMqkLds<T> ? 2 * kImg<T> : kVecLds<T>);
 static_assert(kWaves * kHeads * kMaxL * 4 <= kImg<__bf16>, "head partials fit a free image");
 
 // lane id from an opaque copy of threadIdx.x: per-lane addresses derived from it are recomputed in
@@ -590,14 +595,26 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
   const float* __restrict__ pos = gvecs + kVecSlots * kH;
   constexpr bool kBf16 = sizeof(T) == 2;
   // parameter vectors: LDS copy (bf16) or L2 (fp32)
-  const float* vecs = kBf16 ? reinterpret_cast<const float*>(smem + kOffVec<T>) : gvecs;
-  if constexpr (kBf16) {
+  const float* vecs = (kBf16 && !kMqkLds<T>) ? reinterpret_cast<const float*>(smem + kOffVec<T>) : gvecs;
+  [[maybe_unused]] char* imgq = smem + kOffVec<T>;          // kMqkLds: mq, mk images
+  [[maybe_unused]] char* imgk = smem + kOffVec<T> + kImg<T>;
+  if constexpr (kBf16 && !kMqkLds<T>) {
     float4* dst = reinterpret_cast<float4*>(smem + kOffVec<T>);
     for (int i = threadIdx.x; i < kVecSlots * kH / 4; i += kThreads) dst[i] = reinterpret_cast<const float4*>(gvecs)[i];
   }
   const T* __restrict__ hist = static_cast<const T*>(p.hist);
   const int L = p.L;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto tile_load = [&](char* img, f32x16 (&v)[2]) {         // this wave's column tile, both row tiles
+    const int lane = fresh_lane();
+    const int r = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      Frag<T> f;
+      img_load<T>(f, img, 32 * mt + r, wave, hh);
+      v[mt] = frag_f32<T>(f);
+    }
+  };
   if ((p.abl & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   FF_STAMP_DECL
   int n_done = 0;
@@ -667,7 +684,10 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
     char* oth = img1;
     // the pooler's att_fc1 slabs, loaded during the last layer's G6: all 8 (bf16), so the pooler
     // GEMM issues no load behind the HBM-latency DMA / candidate loads it runs beside
-    constexpr int kPoolPF = kBf16 ? kNS : kPF<T, 1>;
+#ifndef FF_POOL_ALL
+#define FF_POOL_ALL 1
+#endif
+    constexpr int kPoolPF = (kBf16 && FF_POOL_ALL) ? kNS : kPF<T, 1>;
     Frag<T> rp[1][kPoolPF];
 #pragma unroll
     for (int ly = 0; ly < kLayers; ++ly) {
@@ -686,6 +706,10 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       f32x16 mk[2] = {qk[1][0], qk[1][1]};
       add_vec(mq, vecs, vb + lvQB, wave, h);
       add_vec(mk, vecs, vb + lvKB, wave, h);
+      if constexpr (kMqkLds<T>) {        // only this wave reads its tiles back: no barrier
+        tile_store<T>(imgq, mq, wave);
+        tile_store<T>(imgk, mk, wave);
+      }
       if (ly == 0) {
         // pin the ids' scalar loads (issued at the impression start; HBM latency) here, one GEMM
         // later: sunk to their uses they would sit in the lgkmcnt queue beside the LDS reads of
@@ -698,6 +722,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       FF_STAMP(1);
 
       // query attention -> pooled query (model.py:421-433); partials in oth
+      if constexpr (kMqkLds<T>) tile_load(imgq, mq);
       head_partial<T>(reinterpret_cast<float*>(oth), sq, mq, wave);
       __syncthreads();
       FF_STAMP(2);
@@ -705,7 +730,9 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       FF_STAMP(3);
       {
         float pq[16];
+        if constexpr (kMqkLds<T>) tile_load(imgq, mq);
         head_pool(pq, mq, swt, wave);
+        if constexpr (kMqkLds<T>) tile_load(imgk, mk);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {   // mixed_query_key_layer = mk ⊙ pooled query (:436)
           mk[0][e] *= pq[e];
@@ -713,6 +740,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
         }
       }
       // key attention -> pooled key (model.py:439-447); partials in cur (x image dead)
+      if constexpr (kMqkLds<T>) tile_store<T>(imgk, mk, wave);
       head_partial<T>(reinterpret_cast<float*>(cur), sk, mk, wave);
       __syncthreads();
       FF_STAMP(4);
@@ -724,6 +752,10 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       }
       {
         float pk[16];
+        if constexpr (kMqkLds<T>) {
+          tile_load(imgk, mk);
+          tile_load(imgq, mq);
+        }
         head_pool(pk, mk, swt, wave);
         f32x16 wv[2];
 #pragma unroll
@@ -745,6 +777,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
         ring_load<T, 1>(r1, Wn, wave);
       }
       add_vec(t[0], vecs, vb + lvTB, wave, h);
+      if constexpr (kMqkLds<T>) tile_load(imgq, mq);
       t[0][0] += mq[0];
       t[0][1] += mq[1];
       tile_store<T>(cur, t[0], wave);
