@@ -84,6 +84,11 @@ int miner_pack_target_weights(void* stream, int dtype, const void* w_target, int
 
 /*
  * Score B impressions.
+ * dtype MINER_DTYPE_F32 (the reference's precision): the W1·Eᵀ and W2·muiᵀ contractions run as
+ * bf16x6 on the bf16 matrix cores (each fp32 operand cut exactly into three bf16 terms, the six
+ * leading partial products, fp32 accumulation; error vs float64 within 1.5x the fp32 MFMA's), the
+ * rest on the fp32 MFMA; the process environment variable MINER_DENSE_FP32=mfma32, read at each
+ * call, selects every product on the fp32 MFMA (exact fp32 fma chains).
  *   history      [B, L, d]  dtype  clicked-news embeddings, left-padded (reader.py:369)
  *   his_mask     [B, L]     uint8  1 = real click, 0 = pad (entities.py:395)
  *   his_bias     [B, L]     fp32   optional category bias, already averaged over the candidates
