@@ -148,7 +148,32 @@ def host_info():
     except AttributeError:
         aff = None
     return {"threads_used": torch.get_num_threads(), "host_cpus": os.cpu_count(), "affinity_cpus": aff,
-            "cpu_model": model}
+            "quota_cpus": cgroup_cpu_quota(), "cpu_model": model}
+
+
+def cgroup_cpu_quota():
+    """CPUs the container may actually use: the cgroup CPU quota (v2 cpu.max "quota period", v1
+    cfs_quota_us / cfs_period_us), rounded up; None when unlimited or unreadable. The affinity mask
+    can list every CPU of the machine while the quota allows a few of them."""
+    import math
+    for qf, pf in (("/sys/fs/cgroup/cpu.max", None),
+                   ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "/sys/fs/cgroup/cpu/cpu.cfs_period_us"),
+                   ("/sys/fs/cgroup/cpu,cpuacct/cpu.cfs_quota_us", "/sys/fs/cgroup/cpu,cpuacct/cpu.cfs_period_us")):
+        try:
+            with open(qf) as f:
+                parts = f.read().split()
+            if pf is None:
+                quota, period = parts[0], parts[1]
+            else:
+                quota = parts[0]
+                with open(pf) as f:
+                    period = f.read().split()[0]
+            if quota in ("max", "-1") or int(quota) <= 0:
+                return None
+            return max(1, math.ceil(int(quota) / int(period)))
+        except (OSError, ValueError, IndexError):
+            continue
+    return None
 
 
 # ---------------------------------------------------------------------------------------------
@@ -172,9 +197,12 @@ def _batched_oracle_rate(imp, W1, Q, W2, seconds, bs=64):
 
 def cpu_baseline(seconds: float = 15.0, d: int = D):
     """Oracle (torch fp32 CPU restatement of model.py:159-216,127) on host cores, config-3 shape, at
-    two thread counts: the pool's per-GPU CPU share (torch's default here, OMP_NUM_THREADS = 16 on the
-    GPU box) and every CPU of this process's affinity (torch.set_num_threads(os.cpu_count())).
-    ``value`` / ``cores`` are the faster of the two; both are on the line."""
+    the pool's per-GPU CPU share (torch's default here, OMP_NUM_THREADS = 16 on the GPU box) and, when
+    it differs, at the CPUs the container may use: the cgroup CPU quota capped by the affinity mask
+    (SURVEY §8(d) asks for torch.set_num_threads(os.cpu_count()); os.cpu_count() and the affinity
+    list the whole machine — 256 there — and running that many threads on a quota of a few CPUs
+    measured oversubscription, not the CPU: VERDICT r4 item 8). ``value`` / ``cores`` are the faster
+    leg; both legs are on the line."""
     from miner_amd import synthetic
     from oracle import miner_oracle as orc
     hi = host_info()
@@ -182,9 +210,10 @@ def cpu_baseline(seconds: float = 15.0, d: int = D):
     W1, Q, W2 = synthetic.init_weights(36, d, DC, K)
     share = torch.get_num_threads()
     aff = hi["affinity_cpus"] or hi["host_cpus"] or share
+    usable = min(aff, hi["quota_cpus"]) if hi["quota_cpus"] else aff
     legs = {}
     with torch.no_grad():
-        for n_thr in dict.fromkeys([share, aff]):          # one leg when both counts agree
+        for n_thr in dict.fromkeys([share, usable]):       # one leg when both counts agree
             torch.set_num_threads(n_thr)
             rate, pairs, el = _batched_oracle_rate(imp, W1, Q, W2, seconds / 2 if n_thr != share else seconds)
             legs[n_thr] = {"value": round(rate, 1), "threads": n_thr, "seconds": round(el, 1),
@@ -205,12 +234,14 @@ def cpu_baseline(seconds: float = 15.0, d: int = D):
     best = max(legs.values(), key=lambda x: x["value"])
     return {"value": best["value"], "unit": "pairs/s", "cores": best["threads"], "kind": "port",
             "cores_note": f"torch threads of the faster leg; legs: the pool's per-GPU CPU share ({share} threads, "
-                          f"OMP_NUM_THREADS on the GPU box) and all {aff} CPUs of the process affinity "
-                          "(host_cpus is the whole machine)",
+                          f"OMP_NUM_THREADS on the GPU box) and the {usable} CPUs the container may use (cgroup "
+                          f"quota {hi['quota_cpus']} capped by the {aff}-CPU affinity; one leg when equal). "
+                          "host_cpus / affinity_cpus list the whole machine",
             "legs": list(legs.values()),
             "sample": f"{best['impressions']} impressions x {C} candidates (L={L},K={K},d={d},Dc={DC}), fp32, "
                       f"batched 64 impressions/call, {best['seconds']}s",
-            "host_cpus": hi["host_cpus"], "affinity_cpus": hi["affinity_cpus"], "cpu_model": hi["cpu_model"],
+            "host_cpus": hi["host_cpus"], "affinity_cpus": hi["affinity_cpus"], "quota_cpus": hi["quota_cpus"],
+            "cpu_model": hi["cpu_model"],
             "per_candidate_value": round(per_cand, 1),
             "per_candidate_sample": f"{n_imp} impressions, one candidate per sample, batch 32 "
                                     f"(reader.py:376-379 layout), {share} threads, {el2:.1f}s"}

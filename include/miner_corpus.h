@@ -64,8 +64,10 @@ int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mu
                     int32_t* top_ids);
 
 /*
- * The same with a caller-owned device workspace of miner_rank_topk_workspace_bytes(U, topk) bytes
- * (16-byte aligned; NULL: the form above). With it, on a 256-CU device and fewer than 256 two-user
+ * The same with a caller-owned device workspace of workspace_bytes bytes, sized by
+ * miner_rank_topk_workspace_bytes(U, topk) (16-byte aligned; NULL: the form above). The split form
+ * runs only when workspace_bytes covers it, so a workspace sized under another MINER_RK_SPLIT
+ * setting is never overrun (the unsplit form runs instead). With it, on a 256-CU device and fewer than 256 two-user
  * tiles (U <= 510; MINER_RK_SPLIT=1 / 0 forces either form), the news table is split in 8 slices
  * whose per-user top-k lists are merged by a second launch (8x the workgroups for small user
  * batches), the users mapped so that the CUs of one XCD share 8 users' rows in their L2. Same
@@ -75,7 +77,7 @@ int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mu
 size_t miner_rank_topk_workspace_bytes(int U, int topk);
 int miner_rank_topk_ws(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
                        const void* news, int U, int N, int d, int K, int topk, float* top_scores,
-                       int32_t* top_ids, void* workspace);
+                       int32_t* top_ids, void* workspace, size_t workspace_bytes);
 
 #ifdef __cplusplus
 }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MINER_ABI_VERSION 3
+#define MINER_ABI_VERSION 4
 
 /* MINER_DTYPE_F16 is accepted by the full-corpus entry points of miner_corpus.h only (config 5) */
 enum miner_dtype { MINER_DTYPE_F32 = 0, MINER_DTYPE_BF16 = 1, MINER_DTYPE_F16 = 2 };

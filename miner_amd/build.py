@@ -108,5 +108,51 @@ def build_library(force: bool = False, verbose: bool = False, debug: bool = Fals
     return lib
 
 
+ASAN_DRIVER = os.path.join(ROOT, "tests", "native", "abi_errors.cpp")
+
+
+def build_asan_driver(force: bool = False, verbose: bool = False) -> str:
+    """Every csrc/*.hip with AddressSanitizer on its HOST code (``-Xarch_host -fsanitize=address``;
+    the gfx950 device code is built as usual and never runs), linked with
+    tests/native/abi_errors.cpp into build/asan/abi_errors: a CPU program that drives the
+    argument-error paths of every C-ABI entry point (SURVEY §5 sanitizer builds; run by
+    tests/test_asan_abi.py). GPU-side sanitizers are not available on this pool."""
+    from concurrent.futures import ThreadPoolExecutor
+    od = os.path.join(ROOT, "build", "asan")
+    exe = os.path.join(od, "abi_errors")
+    deps = SOURCES + HEADERS + [ASAN_DRIVER]
+    if not force and os.path.exists(exe) and all(os.path.getmtime(exe) >= os.path.getmtime(p) for p in deps):
+        return exe
+    os.makedirs(od, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O1", "-g", "-Xarch_host", "-fsanitize=address", "-fno-omit-frame-pointer",
+             "-std=c++17", "-Wno-pass-failed", "-I", os.path.join(ROOT, "include")]
+
+    def compile_one(src):
+        obj = os.path.join(od, os.path.splitext(os.path.basename(src))[0] + ".o")
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in [src] + HEADERS):
+            return obj
+        lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "c++"]
+        cmd = [hipcc(), *flags, *lang, "-c", src, "-o", obj + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"asan build failed on {os.path.basename(src)}:\n{res.stderr[-4000:]}")
+        os.replace(obj + ".tmp", obj)
+        return obj
+
+    with ThreadPoolExecutor(min(len(SOURCES) + 1, max(1, (os.cpu_count() or 4) // 2))) as ex:
+        objs = list(ex.map(compile_one, SOURCES + [ASAN_DRIVER]))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-fsanitize=address", *objs, "-o", exe + ".tmp"]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"asan link failed:\n{res.stderr[-4000:]}")
+    os.replace(exe + ".tmp", exe)
+    return exe
+
+
 if __name__ == "__main__":
-    print(build_library(force="--force" in sys.argv, verbose=True, debug="--debug" in sys.argv))
+    if "--asan" in sys.argv:
+        print(build_asan_driver(force="--force" in sys.argv, verbose=True))
+    else:
+        print(build_library(force="--force" in sys.argv, verbose=True, debug="--debug" in sys.argv))

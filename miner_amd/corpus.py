@@ -133,6 +133,6 @@ def rank_topk(user_mui: Tensor, user_proj: Optional[Tensor], news: Tensor, topk:
     ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws else None
     with torch.cuda.device(dev):
         rc = _lib.lib().miner_rank_topk_ws(_stream(dev), dt, st, _ptr(mui), _ptr(proj), _ptr(tab), U, N, d, K, topk,
-                                           _ptr(top_s), _ptr(top_i), _ptr(ws))
+                                           _ptr(top_s), _ptr(top_i), _ptr(ws), nws)
     _lib.check(rc, "miner_rank_topk")
     return top_s, top_i

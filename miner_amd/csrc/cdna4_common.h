@@ -198,7 +198,9 @@ __device__ __forceinline__ unsigned hi16_pack(unsigned a, unsigned b) {   // (a 
 __device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
   const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
   hi = hi16_pack(u0, u1);
-  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+  // an infinite x truncates to itself: its residual is 0, not inf - inf (a NaN x stays NaN in mid)
+  const float h0 = __uint_as_float(u0 & 0xffff0000u), h1 = __uint_as_float(u1 & 0xffff0000u);
+  const float r0 = x0 == h0 ? 0.f : x0 - h0, r1 = x1 == h1 ? 0.f : x1 - h1;
   const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
   mid = hi16_pack(v0, v1);
   const float q0 = r0 - __uint_as_float(v0 & 0xffff0000u), q1 = r1 - __uint_as_float(v1 & 0xffff0000u);

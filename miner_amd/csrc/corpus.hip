@@ -445,6 +445,7 @@ struct RkParams {
   int32_t* top_i;
   float* ws_s;             // S > 1: per (user, news slice) top-k lists [U][S][topk], merged by rk_merge
   int32_t* ws_i;
+  size_t ws_bytes;         // the caller's workspace size (the split form needs U·S·topk·8)
   int U, N, d, K, topk, score_type;
 };
 
@@ -922,8 +923,11 @@ bool rk_split_wanted(int U) {
   if (ev && (ev[0] == '0' || ev[0] == '1')) return ev[0] == '1';
   return (U + kUT - 1) / kUT < num_cus();
 }
+size_t rk_ws_bytes(int U, int topk) { return (size_t)U * kSplit * topk * 8; }
+// the split form runs only on a workspace the caller says is large enough for it (the variable may
+// change between the size query and the launch; the launch never trusts the query's answer)
 bool rk_split(const RkParams& prm) {
-  if (prm.ws_s == nullptr || prm.ws_i == nullptr) return false;
+  if (prm.ws_s == nullptr || prm.ws_i == nullptr || prm.ws_bytes < rk_ws_bytes(prm.U, prm.topk)) return false;
   return rk_split_wanted(prm.U);
 }
 
@@ -1051,18 +1055,18 @@ int miner_encode_users(void* stream, int dtype, const void* history, const int32
 size_t miner_rank_topk_workspace_bytes(int U, int topk) {
   if (U <= 0 || topk <= 0 || topk > kMaxTopk) return 0;
   if (!rk_split_wanted(U)) return 0;     // the unsplit form needs no workspace
-  return (size_t)U * kSplit * topk * 8;
+  return rk_ws_bytes(U, topk);
 }
 
 int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
                     const void* news, int U, int N, int d, int K, int topk, float* top_scores, int32_t* top_ids) {
   return miner_rank_topk_ws(stream, dtype, score_type, user_mui, user_proj, news, U, N, d, K, topk, top_scores, top_ids,
-                            nullptr);
+                            nullptr, 0);
 }
 
 int miner_rank_topk_ws(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
                        const void* news, int U, int N, int d, int K, int topk, float* top_scores, int32_t* top_ids,
-                       void* workspace) {
+                       void* workspace, size_t workspace_bytes) {
   const int ck = check_dims(dtype, d, 1, K);
   if (ck != MINER_OK) return ck;
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_MEAN) return MINER_EINVAL;
@@ -1076,6 +1080,7 @@ int miner_rank_topk_ws(void* stream, int dtype, int score_type, const void* user
   if (!aligned16(workspace)) return MINER_EALIGN;
   prm.mui = user_mui; prm.proj = user_proj; prm.news = news; prm.top_s = top_scores; prm.top_i = top_ids;
   if (workspace) {
+    prm.ws_bytes = workspace_bytes;
     prm.ws_s = static_cast<float*>(workspace);
     prm.ws_i = reinterpret_cast<int32_t*>(static_cast<char*>(workspace) + (size_t)U * kSplit * topk * 4);
   }

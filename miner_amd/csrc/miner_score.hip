@@ -93,6 +93,7 @@ struct Params {
   int n_news;
   int eimg;     // bytes of the history image (bf16): the candidate rows may be staged there
   int dbg;      // ablation bits, honoured only by the -DMINER_STAMPS diagnostic build
+  int part_ok;  // fp32: the mui region holds the S6 partial slabs (plain-store reduce); else LDS atomics
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -851,7 +852,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           // fp32: the last chunk (TAA: every chunk) reduces through the dead mui region with plain
           // stores like bf16; the earlier chunks of a C > 64 impression still read mui, so they sum
           // into Lg / Mt with LDS atomics (~190 cycles each: 18 % of the kernel when every chunk did)
-          const bool plain = kBf16 || MODE == kTaa || cc + kCChunk >= Cb;
+          const bool plain = kBf16 || (p.part_ok && (MODE == kTaa || cc + kCChunk >= Cb));
           if (!kBf16 && plain) __syncthreads();   // every wave's mui reads (S6 products) done
           if (plain) {
             s6_reduce_bf16(part, lg, mt, wave, r, h, DBG(3));
@@ -880,7 +881,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           const int c = cc + cl;
           const bool cval = c < Cb;
           float lgv[4], mtv[4];
-          if (kBf16 || MODE == kTaa || cc + kCChunk >= Cb) {
+          if (kBf16 || (p.part_ok && (MODE == kTaa || cc + kCChunk >= Cb))) {
             s7_load_bf16(part, cl, sub, lgv, mtv);
           } else {
 #pragma unroll
@@ -962,6 +963,7 @@ inline int round16(int x) { return (x + 15) & ~15; }
 
 struct Carve {
   int MS, PS, offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux, eimg, total;
+  int part_ok;
 };
 
 // LDS carve (bytes).
@@ -981,7 +983,12 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   const int r2a = 32 * c.MS;
   int r2b = bf ? n_ctiles(Dc) * kSPTile * 4 : pbytes + kMaxK * kMaxL * 4;
   if (parts > r2b) r2b = parts;            // the S6 partial slabs live here too (after the mui reads)
-  const int r2 = round16(mode == kFull ? (r2a > r2b ? r2a : r2b) : (r2a > parts ? r2a : parts));
+  // TAA keeps its mui region at r2a (bf16 TAA has its partial slabs in front of mui, r1). fp32 TAA
+  // reduces through it with plain stores only where it holds the slabs (d >= ~570); below, the
+  // chunks sum with LDS atomics, so the carve (and the two workgroups per CU it allows at small d)
+  // does not grow
+  const int r2 = round16(mode == kFull ? (r2a > r2b ? r2a : r2b) : r2a);
+  c.part_ok = bf || mode == kFull || r2a >= parts;
   const int aw = mode == kFull ? (bf ? 32 * 72 * 2 : 32 * 68 * 4) : 0;
   int off = 0;
   if (bf) {
@@ -1058,7 +1065,7 @@ int run(void* stream, int dtype, int mode, Params prm) {
   const Carve c = carve(dtype, mode, prm.L, prm.d, prm.Dc);
   prm.MS = c.MS; prm.PS = c.PS; prm.offE = c.offE; prm.offZ = c.offZ; prm.offP = c.offP; prm.offS = c.offS;
   prm.offMui = c.offMui; prm.offAw = c.offAw; prm.offPart = c.offPart; prm.offLg = c.offLg; prm.offMt = c.offMt;
-  prm.offAux = c.offAux; prm.eimg = c.eimg;
+  prm.offAux = c.offAux; prm.eimg = c.eimg; prm.part_ok = c.part_ok;
   const bool gather = prm.his_ids != nullptr;
   if (dtype == MINER_DTYPE_BF16) {
     // config 3's model (d = 768, history 50, Dc = 200, K = 32), dense rows: the shape compile-time

@@ -207,8 +207,9 @@ __device__ __forceinline__ uint2 lds_u64(const char* p) { return *reinterpret_ca
 // carried to first order (x·log2 e = yh + yl, yl from one fma and log2 e's low part; e^x =
 // 2^yh·(1 + yl·ln 2)), a few ulp like libm expf in 6 VALU instead of ~14 (its range reduction and
 // over/underflow selects); x is clamped at -104 (e^-104 underflows to 0 either way), so -inf gives 0
+// and a NaN propagates
 __device__ __forceinline__ float x2_exp(float x) {
-  x = fmaxf(x, -104.0f);
+  x = x < -104.0f ? -104.0f : x;                    // not fmaxf: a NaN logit stays NaN (torch softmax)
   const float yh = x * 1.4426950408889634f;
   const float yl = __builtin_fmaf(x, 1.925963033500011e-8f, __builtin_fmaf(x, 1.4426950408889634f, -yh));
   const float e = __builtin_amdgcn_exp2f(yh);

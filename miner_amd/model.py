@@ -11,8 +11,12 @@ plus ``Miner.score(...)``, the entry point after the news encoder (the reference
 method: ``forward`` = news encoder + ``score``). All arithmetic of the scoring path runs in the
 fused HIP kernel; calling these modules with CPU tensors raises (no CPU fallback).
 
-``precision`` selects the kernel mode: ``"fp32"`` (default; exact fp32 arithmetic, parity with the
-reference to 1e-5) or ``"bf16"`` (bf16 operands, fp32 accumulation; the throughput mode).
+``precision`` selects the kernel mode: ``"fp32"`` (default; parity with the reference to 1e-5) or
+``"bf16"`` (bf16 operands, fp32 accumulation; the throughput mode). Since round 4 the fp32 mode runs
+its two large products (S1 ``W1·Eᵀ`` and S5 ``W2·muiᵀ``) as bf16x6: every fp32 operand cut exactly
+into three bf16 terms, the six leading partial products on the bf16 matrix cores (error against
+float64 within 1.5x the fp32 MFMA's, tests/test_gpu_parity.py); ``MINER_DENSE_FP32=mfma32`` selects
+the exact fp32 fma chains of ``v_mfma_f32_32x32x2_f32`` for every product.
 """
 from __future__ import annotations
 

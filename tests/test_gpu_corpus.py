@@ -152,6 +152,35 @@ def test_split_equals_unsplit(dtype, U, N, topk, monkeypatch):
             assert (a[1][:, N:] == -1).all()
 
 
+def test_split_needs_its_workspace(monkeypatch):
+    """The launch takes the split form only on a workspace whose stated size covers it: a buffer
+    sized under another MINER_RK_SPLIT setting (here one 8-byte pair short) runs the unsplit form
+    and is left untouched (the size query and the launch may see different settings)."""
+    import ctypes
+    from miner_amd import _lib
+    gen = torch.Generator().manual_seed(11)
+    U, N, K, d, topk = 37, 3000, 64, 768, 20
+    mui = (torch.randn(U, K, d, generator=gen) / 4).to(DEV, torch.float16)
+    proj = (torch.randn(U, K, d, generator=gen) / 4).to(DEV, torch.float16)
+    tab = (torch.randn(N, d, generator=gen) / d ** 0.5).to(DEV, torch.float16)
+    monkeypatch.setenv("MINER_RK_SPLIT", "0")
+    ref_s, ref_i = corpus.rank_topk(mui, proj, tab, topk)
+    monkeypatch.setenv("MINER_RK_SPLIT", "1")
+    lib = _lib.lib()
+    need = int(lib.miner_rank_topk_workspace_bytes(U, topk))
+    assert need > 0
+    ws = torch.full((need,), 0x5A, dtype=torch.uint8, device=DEV)
+    ts = torch.empty(U, topk, device=DEV)
+    ti = torch.empty(U, topk, dtype=torch.int32, device=DEV)
+    rc = lib.miner_rank_topk_ws(torch.cuda.current_stream().cuda_stream, 2, 0, mui.data_ptr(), proj.data_ptr(),
+                                tab.data_ptr(), U, N, d, K, topk, ts.data_ptr(), ti.data_ptr(), ws.data_ptr(),
+                                ctypes.c_size_t(need - 8))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert bool((ws == 0x5A).all()), "undersized workspace was written"
+    assert torch.equal(ts, ref_s) and torch.equal(ti, ref_i)
+
+
 @pytest.mark.parametrize("K", [64, 32])
 @pytest.mark.parametrize("score_type", ["weighted", "max", "mean"])
 def test_16bit_one_chunk_rows(K, score_type):

@@ -334,6 +334,30 @@ def test_masked_slot_groups(dtype, monkeypatch):
     _ok(s_plain, ref_plain, dtype, "plain scores")
 
 
+def test_x2_nan_logit_propagates(monkeypatch):
+    """A NaN in a clicked slot's logit (here through the category bias) makes the reference's softmax
+    over the history NaN for that impression (torch softmax propagates it, model.py:176-181), so every
+    score of the impression is NaN; the x2 kernel's exp clamp must not turn it into a zero weight
+    (fmaxf(NaN, -104) = -104). The other impressions stay at the fp32 bar."""
+    monkeypatch.setenv("MINER_NEWS_FP32", "x2")
+    B, L = 64, 50
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(21, B, L, 768, 2000, torch.float32)
+    mask[:, -1] = True                                   # the last slot is a click in every impression
+    bias = (torch.rand(hid.shape, device=DEV) - 0.5)
+    bad = torch.tensor([3, 17, 40], device=DEV)
+    bias[bad, -1] = float("nan")
+    nt = news.precompute(table, W1, Q, W2)
+    s = news.score(nt, hid, mask, cid, his_bias=bias)
+    torch.cuda.synchronize()
+    _, ref = _oracle(table, hid, mask, cid, None, W1, Q, W2, bias=bias)
+    s, ref = s.cpu().reshape(B, -1), ref.reshape(B, -1)
+    assert torch.isnan(ref[bad.cpu()]).all()
+    assert torch.equal(torch.isnan(s), torch.isnan(ref)), "NaN pattern differs from the reference"
+    keep = torch.ones(B, dtype=torch.bool)
+    keep[bad.cpu()] = False
+    _ok(s[keep], ref[keep], torch.float32, "finite impressions")
+
+
 def test_mui_only_and_all_padded():
     table, hid, mask, cid, offs, W1, Q, W2 = _setup(8, 50, 30, 256, 500, torch.float32)
     mask[:10] = False                      # all-padded histories: uniform average of pad rows

@@ -113,7 +113,10 @@ def main():
         gui = med["GRBM_GUI_ACTIVE"] / args.xcds
         res["gpu_busy_cycles"] = gui
         res["mfma_busy_frac"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui * 4 * args.cus)
-        res["mfma_instructions_32x32x16"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / 32
+        # SQ_VALU_MFMA_BUSY_CYCLES counts matrix-pipe cycles (32 per v_mfma_f32_32x32x16_bf16, 16 per
+        # 16x16x32 f16/bf16, 64 per 32x32x2_f32, 32 per 16x16x4_f32): expressed in 16-cycle units,
+        # which is the instruction count for the 16x16x32 kernels (news_score_x2, news_score<bf16>)
+        res["mfma_busy_16cycle_units"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / 16
     for c in sorted(med):
         if c.startswith(("SQ_", "GRBM_")) and c not in res:
             res[c] = med[c]

@@ -50,13 +50,14 @@ def run(variants, U=2048, N=200000, reps=3):
     libs = {}
     for v in variants:
         h = ctypes.CDLL(os.path.join(OUT, f"librk_abl{v.rstrip('sg')}.so"))
-        h.miner_rank_topk_ws.argtypes = [P, I, I, P, P, P, I, I, I, I, I, P, P, P]
+        h.miner_rank_topk_ws.argtypes = [P, I, I, P, P, P, I, I, I, I, I, P, P, P, ctypes.c_size_t]
         libs[v] = h
 
     def launch(v):
         os.environ["MINER_RK_GEO"] = "1" if "g" in v else "0"
         rc = libs[v].miner_rank_topk_ws(st, 2, 0, mui.data_ptr(), proj.data_ptr(), table.data_ptr(), U, N, d, K, topk,
-                                        ts.data_ptr(), ti.data_ptr(), ws.data_ptr() if v.endswith("s") else None)
+                                        ts.data_ptr(), ti.data_ptr(), ws.data_ptr() if v.endswith("s") else None,
+                                        ws.numel() if v.endswith("s") else 0)
         assert rc == 0, rc
 
     times = {v: [] for v in variants}
