@@ -619,6 +619,7 @@ def run_news(args, rank, world, dev):
     c2 = config2_line(args, rank, world, dev) if not args.no_config2 else None
     c4 = config4_subline(dev) if (world == 1 and not args.no_config2) else None
     c5 = config5_subline(dev) if (world == 1 and not args.no_config2) else None
+    wide = wide_news_subline(dev) if (world == 1 and not args.no_config2) else None
 
     if rank != 0:
         return
@@ -673,7 +674,8 @@ def run_news(args, rank, world, dev):
                        "flops": pre_fl, "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
                        "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
         "fp32_mfma_exact": exact, "eval_with_loss": loss_line, "full_histories": full_hist, "weak_scaling": weak,
-        "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "metric_step": metric_step,
+        "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "wide_news": wide,
+        "metric_step": metric_step,
         "dense_rows_kernel": dense, "with_host_tolist": with_host,
         "cpu_baseline": cpu, "auc_parity": auc, "pmc_status": PMC_STATUS,
     }
@@ -937,6 +939,65 @@ def config4_subline(dev, steps=5, warmup=2):
             "impressions_per_step": FF_B, "ms_per_step": round(ms, 4), "steps": steps,
             "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "kernel": "ff_fused<bf16>"}}
+
+
+WN_B, WN_L, WN_K = 100_000, 100, 64      # the wide news-id line: K = 64, L = 100
+
+
+def wide_news_subline(dev, steps=5, warmup=2):
+    """A reference-legal model past the news kernels' K <= 32 / L <= 64 (model.py:18-21, :159-185):
+    K = 64 interests, history 100, d = 768, 40 candidates, 100k impressions as news ids over the
+    104k-news table (left padding = the pad news, as news_batch). The news-id path (per-news
+    precompute, logits in 32-interest slices + news_score_x2w, fp32 on the fp16 matrix cores)
+    against the wide path it replaces (miner_encode_users + miner_score_wide, exact fp32, recomputing
+    gelu(mui·W2ᵀ) per user), the latter on the first 20k impressions."""
+    from miner_amd import news, ops, synthetic
+    g = torch.Generator(device=dev).manual_seed(64)
+    table = torch.randn((N_NEWS, D), generator=g, device=dev) / D ** 0.5
+    W1, Q, W2 = synthetic.init_weights(64, D, DC, WN_K, device=dev)
+    pos = torch.arange(WN_L, device=dev)
+    lens = torch.randint(0, WN_L + 1, (WN_B,), generator=g, device=dev)
+    mask = pos[None, :] >= (WN_L - lens)[:, None]
+    hid = torch.where(mask, torch.randint(1, N_NEWS, (WN_B, WN_L), generator=g, device=dev, dtype=torch.int32),
+                      torch.zeros((), dtype=torch.int32, device=dev))
+    cid = torch.randint(1, N_NEWS, (WN_B, C), generator=g, device=dev, dtype=torch.int32)
+    nt = [news.precompute(table, W1, Q, W2, x2=True)]
+    out = [None]
+
+    def pre():
+        nt[0] = news.precompute(table, W1, Q, W2, out=nt[0], x2=True)
+
+    def fn():
+        out[0] = news.score(nt[0], hid, mask, cid, validate=False, x2=True)
+
+    pre_ms = _kernel_ms(pre, 2, 1, dev)
+    ms = _kernel_ms(fn, steps, warmup, dev)
+    assert torch.isfinite(out[0]).all()
+    Bo = 20_000
+    pw = ops.pack_weights(W1, Q, W2)
+    old = [None]
+
+    def fn_old():
+        old[0] = ops.score_gather(table, hid[:Bo], mask[:Bo], cid[:Bo], pw, validate=False)
+
+    ms_old = _kernel_ms(fn_old, 2, 1, dev)
+    d_old = float((old[0].double() - out[0][:Bo].double()).abs().max() / old[0].double().pow(2).mean().sqrt())
+    byt = bytes_per_impression(WN_L, D, C, 4) * WN_B
+    gbs = byt / (ms / 1e3) / 1e9
+    return {"workload": f"K={WN_K}, history {WN_L}, d={D}, {C} candidates, {WN_B} impressions as news ids "
+                        f"({N_NEWS}-news table), fp32",
+            "value": round(WN_B * C / (ms / 1e3), 1), "unit": "pairs/s", "dtype": "fp32",
+            "kernel": "news_score_x2w<weighted, dense> (fp16-pair operands)", "ms_per_launch": round(ms, 4),
+            "steps": steps, "precompute_ms": round(pre_ms, 3),
+            "value_with_precompute": round(WN_B * C / ((ms + pre_ms) / 1e3), 1),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4),
+                         "algorithmic_bytes_per_impression": bytes_per_impression(WN_L, D, C, 4)},
+            "replaced_wide_path": {"kernels": "ue_fused<fp32> + wide_score<fp32> (miner_encode_users + "
+                                              "miner_score_wide)", "impressions": Bo,
+                                   "value": round(Bo * C / (ms_old / 1e3), 1), "unit": "pairs/s",
+                                   "ms_per_launch": round(ms_old, 3),
+                                   "max_abs_diff_x_rms": d_old}}
 
 
 def config5_subline(dev, steps=2, warmup=1):

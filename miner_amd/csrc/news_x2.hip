@@ -66,6 +66,21 @@ namespace {
 #ifndef X2_DMA_EARLY
 #define X2_DMA_EARLY 1 // the next chunk's row DMAs issued right after the barrier, before a pass start's S7 / softmax / aux work
 #endif
+#ifndef X2_PIPE
+#define X2_PIPE 0      // (measured +6 %, r05) the per-impression work spread over the chunks of the previous impression (compile-time chunk counts >= 4, no eval loss)
+#endif
+#ifndef X2_S7_LATE
+#define X2_S7_LATE 0   // A/B: S7 of the previous pass at a pass's second chunk instead of its first
+#endif
+#ifndef X2_DEDUPE_WAVE
+#define X2_DEDUPE_WAVE 7 // A/B: the wave that runs the dedupe (PIPE: 3)
+#endif
+#ifndef X2_M0CLOB
+#define X2_M0CLOB 0    // A/B: the row DMAs leave M0 set (declared clobbered) instead of saving / restoring it
+#endif
+#ifndef X2_MERGE_EARLY
+#define X2_MERGE_EARLY 1 // the dedupe's unit merge right after a barrier, before the chunk's row DMAs are issued (its compiler wait then costs nothing)
+#endif
 constexpr int kNB = 2;                                 // row-DMA blocks per wave per part
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
@@ -129,6 +144,11 @@ __device__ __forceinline__ float x_rows4_sum(float x) {
 
 // one row DMA (saddr form: scalar base + 32-bit per-lane offset) into M0 = m, M0 saved / restored
 __device__ __forceinline__ void x2_dma_row(uint32_t off, const char* base, unsigned m) {
+#if X2_M0CLOB
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(off), "s"(base), "s"(__builtin_amdgcn_readfirstlane(m)) : "memory", "m0");
+  return;
+#endif
   unsigned t;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
                "s_mov_b32 m0, %0"
@@ -342,6 +362,18 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   const float* const bias = SHP == 2 ? nullptr : p.bias;
   float* const mui_out = SHP == 2 ? nullptr : p.mui_out;
   float* const dis_out = LOSS ? p.dis_out : nullptr;
+  // PIPE: impression ci's per-impression work runs spread over the chunks of pass 0 of impression
+  // ci - 1 (schedule below), so no chunk carries all of it and the row stream keeps flowing; the
+  // dedupe then moves to a mui wave (the X waves run S7)
+  constexpr bool PIPE = X2_PIPE && !LOSS && NCH >= 4;
+  constexpr int kDedupeWave = PIPE ? 3 : X2_DEDUPE_WAVE;
+  constexpr bool S7LATE = X2_S7_LATE && !PIPE && !LOSS && NCH >= 3;
+  constexpr int cS7 = 1;                               // S7 of the previous pass (X waves), every pass
+  constexpr int cDED = NCH >= 8 ? 2 : 1;               // unit merge + dedupe of ci + 2 (wave 3), L0 / L1 aux DMAs
+  constexpr int cL2 = cDED + 1;                        // logit rows of ci + 2 (after its dedupe)
+  constexpr int cSM0 = NCH >= 8 ? cL2 + 1 : cL2;       // softmax of ci + 1, mui waves (after ci + 1's unit merge at cDED)
+  constexpr int cSM1 = NCH >= 8 ? cSM0 + 2 : NCH - 1;  // softmax of ci + 1, X waves
+  static_assert(!PIPE || (cSM0 > cDED && cSM1 > cDED && cSM1 < NCH && cS7 < NCH - 1), "x2 chunk schedule");
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = wave >> 2, ch = (wave >> 1) & 1, kt = wave & 1;
   const bool k_live = 16 * kt < KK;
@@ -422,15 +454,22 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // impressions after their dedupe). Wave 7 only; du_i = the impression whose units are pending.
   float du_E = 1.f, du_P = 1.f;
   int du_slot = -1, du_i = -1;
-  auto dedupe_prep = [&](int i) {
-    if (wave != 7) return;
-    const int l = threadIdx.x & 63;
+  // the merge of the pending units: the compiler waits for their loads here (vmcnt), so it is called
+  // right after a barrier (X2_MERGE_EARLY), when this wave's row DMAs have all landed, not behind the
+  // chunk DMAs it has just issued
+  auto dedupe_merge = [&]() {
+    if (wave != kDedupeWave) return;
     if (du_i >= 0) {
       int* pcp = reinterpret_cast<int*>(prep_blk(smem, du_i));
       if (du_slot >= 0)
         pcp[du_slot] |= (((__float_as_int(du_E) >> 23) & 255) << 8) | (((__float_as_int(du_P) >> 23) & 255) << 16);
       du_i = -1;
     }
+  };
+  auto dedupe_prep = [&](int i) {
+    if (wave != kDedupeWave) return;
+    const int l = threadIdx.x & 63;
+    dedupe_merge();
     if (i >= n_i) return;
     int* his = l1_his(smem, i & 3);
     const int ls = min(l, L - 1);
@@ -549,6 +588,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kt + i][u] of the history
   // groups u = 32 kb + 16 (e >> 2) + 4g + (e & 3) (aH1 / aL1: interest tile 1, the Gram waves only)
   u32x4 aH[2], aL[2], aH1[2], aL1[2];
+  u32x4 aHn[2], aLn[2];                    // PIPE: the next impression's, computed a few chunks ahead
+  float kapn = kSA;
+  int nkb_n = 2;
 
   // softmax over the history groups (model.py:176-181) of this wave's 16 interests, in registers:
   // lane (g, i) takes 16 groups, the 4 lane rows combined by permlanes
@@ -831,6 +873,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     else compute_t(ci, cc, mode, integral_constant<int, 1>{});
   };
 
+  if constexpr (PIPE) {                          // impression 0's attention weights (the rest: a chunk schedule ahead)
+    using std::integral_constant;
+    if (n_i > 0) {
+      const int nkb0 = __builtin_amdgcn_readfirstlane(dup_u(smem, 0)[0]) > 32 ? 2 : 1;
+      if (X2_SOFT_HALF && nkb0 == 1) softmax_inwave(0, kt, P, aH, aL, kap, integral_constant<int, 8>{});
+      else softmax_inwave(0, kt, P, aH, aL, kap, integral_constant<int, 16>{});
+    }
+  }
   // static priority for the X waves 4-7 (the GELU chain)
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   for (int ci = 0; ci < n_i; ++ci) {
@@ -862,11 +912,47 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
             dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
           }
         };
+        // the unit merge waits (compiler vmcnt) for the loads of the previous dedupe: here, before
+        // this chunk's DMAs are issued, they have landed and the wait is free
+        if (X2_MERGE_EARLY && (!LOSS || SHP == 2) && cp == 0 && cc == (PIPE ? cDED : 0)) dedupe_merge();
         if (X2_DMA_EARLY) issue_next();
-        if (cc == 0) {
+        if constexpr (PIPE) {
+          if (cc == 0) {
+            if (cp == 0 && ci > 0) {       // the A fragments of this impression, computed during the last
+#pragma unroll
+              for (int kb = 0; kb < 2; ++kb) {
+                aH[kb] = aHn[kb];
+                aL[kb] = aLn[kb];
+              }
+              kap = kapn;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          if (cc == cS7) {
+            if (WITH_CAND && pend_off >= 0) s7();
+            pend_off = -1;
+          }
+          if (cp == 0) {
+            if (cc == cDED) {
+              dedupe_prep(ci + 2);         // L1 of ci + 2 landed; its logit rows are DMA'd by group next
+              issue_L0(ci + 4);
+              issue_L1(ci + 3);
+            }
+            if (cc == cL2) issue_L2(ci + 2);   // into the block impression ci's logits were read from
+            if (((cc == cSM0 && P == 0) || (cc == cSM1 && P == 1)) && ci + 1 < n_i) {
+              using std::integral_constant;
+              nkb_n = __builtin_amdgcn_readfirstlane(dup_u(smem, (ci + 1) & 3)[0]) > 32 ? 2 : 1;
+              if (X2_SOFT_HALF && nkb_n == 1) softmax_inwave(ci + 1, kt, P, aHn, aLn, kapn, integral_constant<int, 8>{});
+              else softmax_inwave(ci + 1, kt, P, aHn, aLn, kapn, integral_constant<int, 16>{});
+            }
+          }
+        } else if (cc == 0) {
           did_s7 = (WITH_CAND && pend_off >= 0) || d_pending;
-          if (WITH_CAND && pend_off >= 0) s7();
-          pend_off = -1;
+          if (!S7LATE) {
+            if (WITH_CAND && pend_off >= 0) s7();
+            pend_off = -1;
+          }
           if (LOSS && pend_d >= 0) form_d(pend_d);
           pend_d = -1;
           d_pending = false;
@@ -891,6 +977,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
         } else if (cc == 1 && cp == 0) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
+        }
+        if (S7LATE && cc == 1) {
+          if (WITH_CAND && pend_off >= 0) s7();
+          pend_off = -1;
         }
         X2_STAMP(2);
         if (!X2_DMA_EARLY) issue_next();
@@ -959,6 +1049,563 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 }
 
 // ================================================================================================
+// wide shapes: K <= 64 interests, L <= 128 history slots (news_score_x2w)
+// ================================================================================================
+// The reference limits neither num_context_codes (model.py:18-21) nor the history length
+// (model.py:159-185); news_score_x2's LDS carve stops at K <= 32, L <= 64. news_score_x2w is the
+// same math on the same pair planes and per-news precompute, laid out for K <= 64 and up to 128
+// history groups:
+//   - 32-column steps: one 128-byte piece per row (32 hi | 32 lo fp16 of the 64-column chunk),
+//     two LDS slots [E[his] 128 rows | proj[his] 128 rows | Cand 64 rows], LDS-DMA by id one step
+//     ahead, one barrier per step; rows past the groups / the candidate count are not fetched;
+//   - wave w = (path P = w >> 2, interest tile kq = w & 3): muiᵀ / Xᵀ [32 cols x 16 interests] =
+//     part[his]ᵀ·Aᵀ over up to 4 history blocks of 32 (the history operand read transposed, Aᵀ pairs
+//     in registers), then M / Lg [16 cands x 16 interests] += Cand·muiᵀ / Xᵀ per candidate tile;
+//   - per impression, at its first step: the softmax over the history groups (each wave, its 16
+//     interests), S7 of the previous pass (X waves, 16 candidates x 16 interests per lane row) and
+//     the dedupe of the next impression (wave 7); the logit rows of the next impression land in
+//     the single logit block at the second step.
+// The masked slots holding the first masked slot's news id form one group (as news_score_x2).
+constexpr int kWMaxL = 128;
+constexpr int kWMaxK = 64;
+constexpr int kWRB = 128;                              // bytes per staged row piece (32 hi | 32 lo)
+constexpr int kWPart = kWMaxL * kWRB;                  // 128 rows
+constexpr int kWCTile = 16 * kWRB + 16;                // candidate tiles 16 B apart (see kCTile)
+constexpr int kWSlot = 2 * kWPart + 4 * kWCTile;
+constexpr int kWRing = 2 * kWSlot;
+constexpr int kWOffF = kWRing;                         // F[P] [c 64][k ^ (c & 15)] fp32
+constexpr int kWFB = 2 * 64 * 64 * 4;
+constexpr int kWOffLog = kWOffF + kWFB;                // logit rows of one impression [group][64]
+constexpr int kWLogB = kWMaxL * kWMaxK * 4;
+constexpr int kWOffL1 = kWOffLog + kWLogB;             // 3 slots: his ids | mask words | bias | cand ids
+constexpr int kWL1B = 3 * 4 * kWMaxL + 4 * kMaxCand;
+constexpr int kWOffL0 = kWOffL1 + 3 * kWL1B;           // 8 slots: CSR offsets (ragged)
+constexpr int kWOffPrep = kWOffL0 + 8 * kL0B;          // 2 blocks: code[128] | add[128]
+constexpr int kWPrepB = 2 * kWMaxL * 4;
+constexpr int kWOffDup = kWOffPrep + 2 * kWPrepB;      // per L1 slot: U
+constexpr int kWLds = kWOffDup + 3 * kDupB;
+static_assert(kWLds <= 160 * 1024, "news_score_x2w LDS");
+
+// 16-byte chunk swizzle of a staged 128-byte row (8 chunks: hi 0..3, lo 4..7): slot = chunk ^
+// wswz(row). Over the 4 same-parity rows of a transposed read's 8-row group it takes the even
+// values {0, 2, 4, 6} (rows 8..15 of a 16: the odd ones), so the chunk pairs of the two lanes'
+// column halves land in 8 different slots; over the 8 same-parity rows of a 16-row candidate tile
+// all 8 values: both reads are conflict-free (ds_read_b64 / _tr_b16 bank over 256 B per 32 lanes)
+__host__ __device__ inline int wswz(int row) { return (((row >> 1) & 3) << 1) | ((row >> 3) & 1); }
+
+template <int ST, bool RAGGED>
+__global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
+  constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
+  const int G = gridDim.x;
+  const int n_i = (p.B - (int)blockIdx.x + G - 1) / G;
+  const int L = p.L, KK = p.K, d = p.d;
+  const int nst = d >> 5;                                 // 32-column steps
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int P = wave >> 2, kq = wave & 3;
+  const bool k_live = 16 * kq < KK;
+  const bool path_live = P == 0 || WEIGHTED;
+  const char* tabB = static_cast<const char*>(p.table2);
+  const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj2) : tabB;
+  const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
+  float kap = kSA;                         // κ_k of this lane's interest (the wave's path), per impression
+  float uc_pend = 1.0f;                    // S7 lane's candidate unit (X waves)
+
+  auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
+  auto l1 = [&](int i) { return smem + kWOffL1 + (i % 3) * kWL1B; };
+  auto w_his = [&](int i) { return reinterpret_cast<int*>(l1(i)); };
+  auto w_mask = [&](int i) { return reinterpret_cast<uint32_t*>(l1(i) + 4 * kWMaxL); };
+  auto w_bias = [&](int i) { return reinterpret_cast<float*>(l1(i) + 8 * kWMaxL); };
+  auto w_cand = [&](int i) { return reinterpret_cast<int*>(l1(i) + 12 * kWMaxL); };
+  auto w_dup = [&](int i) { return reinterpret_cast<int*>(smem + kWOffDup + (i % 3) * kDupB); };
+  auto w_prep = [&](int i) { return reinterpret_cast<float*>(smem + kWOffPrep + (i & 1) * kWPrepB); };
+  auto cands = [&](int i, int& off, int& cnt) {
+    if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
+    if constexpr (RAGGED) {
+      const int* o = reinterpret_cast<const int*>(smem + kWOffL0 + (i & 7) * kL0B);
+      off = __builtin_amdgcn_readfirstlane(o[0]);
+      cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
+    } else {
+      off = imp_b(i) * p.C;
+      cnt = p.C;
+    }
+    cnt = min(max(cnt, 0), kMaxCand);
+  };
+  // ---- aux DMAs: L0 CSR offsets -> L1 ids / mask / bias / candidate ids -> L2 logit rows by group ----
+  auto issue_L0 = [&](int i) {
+    if (RAGGED && wave == 0 && i < n_i && (threadIdx.x & 63) < 2)
+      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kWOffL0 + (i & 7) * kL0B);
+  };
+  auto issue_L1 = [&](int i) {
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const unsigned dst = sbase + (unsigned)(l1(i) - smem);
+    for (int hh = 0; hh < 2 && 64 * hh < L; ++hh) {
+      const size_t base = (size_t)imp_b(i) * L + min(lane + 64 * hh, L - 1);
+      if (wave == 1) {
+        dma_b32(p.his_ids + base, dst + 256 * hh);
+      } else if (wave == 2) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
+        dma_b32(reinterpret_cast<const void*>(a), dst + 4 * kWMaxL + 256 * hh);
+      } else if (wave == 3) {
+        if (p.bias) dma_b32(p.bias + base, dst + 8 * kWMaxL + 256 * hh);
+      }
+    }
+    if (WITH_CAND && wave >= 4) {
+      int off, cnt;
+      cands(i, off, cnt);
+      for (int j = wave - 4; 64 * j < cnt; j += 4) {
+        const int c = min(64 * j + lane, cnt - 1);
+        dma_b32(p.cand_ids + off + c, dst + 12 * kWMaxL + 256 * j);
+      }
+    }
+  };
+  auto issue_L2 = [&](int i) {             // 16-byte pieces of the groups' logit rows, 4 rows per DMA
+    if (i >= n_i) return;
+    const int lane = threadIdx.x & 63;
+    const int U = __builtin_amdgcn_readfirstlane(w_dup(i)[0]);
+    const int* his = w_his(i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = wave + 8 * j;                         // DMA n: rows 4n .. 4n + 3
+      if (4 * n >= U) break;
+      const int row = min(4 * n + (lane >> 4), U - 1);
+      const int pc = min(lane & 15, (KK >> 2) - 1);
+      const int id = min(max(his[row], 0), p.n_news - 1);
+      x2_dma_b128(p.logits + (size_t)id * KK + 4 * pc, sbase + kWOffLog + n * 1024);
+    }
+  };
+  // the groups of impression i (wave 7; two 64-slot halves): its history ids are replaced by the
+  // groups' ids, each group's code (multiplicity, click bit, row-unit exponents) and additive term
+  // written; the units land a step later (dedupe_merge, right after a barrier)
+  float du_E[2] = {1.f, 1.f}, du_P[2] = {1.f, 1.f};
+  int du_slot[2] = {-1, -1}, du_i = -1;
+  auto dedupe_merge = [&]() {
+    if (wave != 7 || du_i < 0) return;
+    int* pcp = reinterpret_cast<int*>(w_prep(du_i));
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      if (du_slot[hh] >= 0)
+        pcp[du_slot[hh]] |= (((__float_as_int(du_E[hh]) >> 23) & 255) << 8) | (((__float_as_int(du_P[hh]) >> 23) & 255) << 16);
+    du_i = -1;
+  };
+  auto dedupe_prep = [&](int i) {
+    if (wave != 7 || i >= n_i) return;
+    const int l = threadIdx.x & 63;
+    int* his = w_his(i);
+    int id[2];
+    bool keep[2], valid[2];
+    float bv[2];
+    unsigned long long pads[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int s = l + 64 * hh;
+      const int ls = min(s, L - 1);
+      valid[hh] = s < L;
+      id[hh] = his[ls];
+      const uint32_t mw = w_mask(i)[ls];
+      const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + ls) & 3);
+      keep[hh] = ((mw >> (8 * a)) & 0xffu) != 0u;
+      bv[hh] = (keep[hh] && p.bias) ? w_bias(i)[ls] : 0.f;
+      pads[hh] = __ballot(valid[hh] && !keep[hh]);
+    }
+    const int f = pads[0] ? (int)__builtin_ctzll(pads[0]) : pads[1] ? 64 + (int)__builtin_ctzll(pads[1]) : 0;
+    const int idf = f >= 64 ? __builtin_amdgcn_readlane(id[1], f - 64) : __builtin_amdgcn_readlane(id[0], f);
+    unsigned long long grp[2], bal[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) grp[hh] = pads[hh] & __ballot(id[hh] == idf);
+    const int mg = __popcll(grp[0]) + __popcll(grp[1]);
+    bool uniq[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const bool ing = ((grp[hh] >> l) & 1ull) != 0ull;
+      uniq[hh] = valid[hh] && (!ing || l + 64 * hh == f);
+      bal[hh] = __ballot(uniq[hh]);
+    }
+    const int U0 = __popcll(bal[0]);
+    const int U = U0 + __popcll(bal[1]);
+    float* pr = w_prep(i);
+    int* pc = reinterpret_cast<int*>(pr);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int uidx = (hh ? U0 : 0) + __popcll(bal[hh] & ((1ull << l) - 1ull));
+      const bool ing = ((grp[hh] >> l) & 1ull) != 0ull;
+      const int idc = min(max(id[hh], 0), p.n_news - 1);
+      du_E[hh] = p.unit_t[idc];
+      du_P[hh] = WEIGHTED ? p.unit_p[idc] : 1.0f;
+      if (uniq[hh]) {
+        his[uidx] = id[hh];
+        pc[uidx] = (ing ? mg : 1) | (keep[hh] ? 1 << 24 : 0);
+        pr[kWMaxL + uidx] = keep[hh] ? bv[hh] : 1e-30f;
+      }
+      du_slot[hh] = uniq[hh] ? uidx : -1;
+      if (l + 64 * hh >= U) {              // past the groups: weight 0, units 2^-14
+        pc[l + 64 * hh] = (113 << 8) | (113 << 16);
+        pr[kWMaxL + l + 64 * hh] = -INFINITY;
+      }
+    }
+    if (l == 0) w_dup(i)[0] = U;
+    du_i = i;
+  };
+
+  // ---- row DMAs of a step: wave w fills history rows 64 jj + 8w .. + 7 of E and proj (jj = 0, 1)
+  // and candidate rows 8w .. 8w + 7; lane l: row 8 blk + (l >> 3), chunk slot l & 7 from source
+  // chunk slot ^ wswz(row) (hi chunks 0..3 at +16 c, lo chunks at +128 + 16 (c - 4) of the
+  // 64-column chunk, the step's half at +64)
+  auto chunk_off = [](int row, int sl) {
+    const int c = sl ^ wswz(row);
+    return (uint32_t)((c & 4) * 32 + 16 * (c & 3));
+  };
+  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t& oC, unsigned& lv) {
+    const int lane = threadIdx.x & 63;
+    const bool live = i < n_i;
+    int off = 0, cnt = 1;
+    if (live) cands(i, off, cnt);
+    const int cntp = max(1, min(64, cnt - 64 * pass));
+    const int U = live ? __builtin_amdgcn_readfirstlane(w_dup(i)[0]) : 1;
+    const uint32_t rowBytes = (uint32_t)d * 4u;
+    lv = 0;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row0 = 64 * jj + 8 * wave;
+      if (live && row0 < U) lv |= 1u << jj;
+      const int row = row0 + (lane >> 3);
+      int h = live ? w_his(i)[min(row, U - 1)] : 0;
+      h = min(max(h, 0), p.n_news - 1);
+      oH[jj] = (uint32_t)h * rowBytes + chunk_off(row, lane & 7);
+    }
+    {
+      const int row = 8 * wave + (lane >> 3);
+      if (live && WITH_CAND && 8 * wave < cnt - 64 * pass) lv |= 16u;
+      int c = (live && WITH_CAND) ? w_cand(i)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)] : 0;
+      c = min(max(c, 0), p.n_news - 1);
+      oC = (uint32_t)c * rowBytes + chunk_off(row, lane & 7);
+    }
+    lv = __builtin_amdgcn_readfirstlane(lv);
+  };
+  auto dma_step = [&](const uint32_t* oH, uint32_t oC, unsigned lv, int sg, int slot) {
+    if (lv == 0) return;
+    const int so = (sg >> 1) * 256 + (sg & 1) * 64;
+    const unsigned m = sbase + slot * kWSlot;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      if (lv & (1u << jj)) {
+        x2_dma_row(oH[jj], tabB + so, m + jj * 8192 + wave * 1024);
+        if (WEIGHTED) x2_dma_row(oH[jj], prjB + so, m + kWPart + jj * 8192 + wave * 1024);
+      }
+    }
+    if (lv & 16u) x2_dma_row(oC, tabB + so, m + 2 * kWPart + (wave >> 1) * kWCTile + (wave & 1) * 1024);
+  };
+
+  // ---- per-lane LDS read offsets (fixed for the launch): as news_score_x2, 128-byte rows ----
+  uint32_t trH[2][2], trL[2][2], cfH[2], cfL[2];
+  {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, i = lane & 15;
+#pragma unroll
+    for (int ctl = 0; ctl < 2; ++ctl) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int row = 16 * rr + 4 * g + q;
+        const int chunk = 2 * ctl + (pp >> 1);
+        trH[ctl][rr] = row * kWRB + ((chunk ^ wswz(row)) << 4) + 8 * (pp & 1);
+        trL[ctl][rr] = row * kWRB + (((chunk + 4) ^ wswz(row)) << 4) + 8 * (pp & 1);
+      }
+      const int chunk = 2 * ctl + (g >> 1);
+      cfH[ctl] = i * kWRB + ((chunk ^ wswz(i)) << 4) + 8 * (g & 1);
+      cfL[ctl] = i * kWRB + (((chunk + 4) ^ wswz(i)) << 4) + 8 * (g & 1);
+    }
+  }
+
+  // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kq + i][u] of the groups
+  // u = 32 kb + 16 (e >> 2) + 4g + (e & 3)
+  u32x4 aH[4], aL[4];
+  int nkb = 4;
+  // softmax over the groups (model.py:176-181) of this wave's 16 interests, in registers (as
+  // news_score_x2's softmax_inwave, up to 32 groups per lane)
+  auto softmax_w = [&](int i, auto nss_c) {
+    constexpr int NSS = decltype(nss_c)::value;   // groups per lane: 16 (<= 64 groups) or 32
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    const int k = 16 * kq + j;
+    const float* lgb = reinterpret_cast<const float*>(smem + kWOffLog);
+    const float* pr = w_prep(i);
+    const int* pc = reinterpret_cast<const int*>(pr);
+    const unsigned sh = P ? 16u : 8u;
+    float v[NSS], wm[NSS], un[NSS];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < NSS; ++s) {
+      const int u = 32 * (s >> 3) + 16 * ((s >> 2) & 1) + 4 * g + (s & 3);
+      const unsigned code = (unsigned)pc[u];
+      wm[s] = (float)(code & 255u);
+      un[s] = __uint_as_float(__builtin_amdgcn_ubfe(code, sh, 8) << 23);
+      const float click = __uint_as_float((code >> 24) * 0x3f800000u);
+      v[s] = __builtin_fmaf(lgb[u * kWMaxK + min(k, KK - 1)], click, pr[kWMaxL + u]);
+      mx = fmaxf(mx, v[s]);
+    }
+    mx = x_rows4_max(mx);
+    float sum = 0.f, tu = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSS; ++s) {
+      v[s] = x2_exp(v[s] - mx);
+      const float we = wm[s] * v[s];
+      sum += we;
+      tu = __builtin_fmaf(we, un[s], tu);
+    }
+    sum = x_rows4_sum(sum);
+    tu = x_rows4_sum(tu);
+    int e;
+    frexpf(tu / sum, &e);
+    e = min(max(e, -100), 114);
+    kap = __int_as_float((141 - e) << 23);
+    float inv = kap / sum;
+    if (k >= KK) inv = 0.f;
+#pragma unroll
+    for (int m = 0; m < NSS / 2; ++m) {
+      unsigned hv, lv2;
+      split2w(wm[2 * m], v[2 * m], inv * un[2 * m], wm[2 * m + 1], v[2 * m + 1], inv * un[2 * m + 1], hv, lv2);
+      aH[m >> 2][m & 3] = hv;
+      aL[m >> 2][m & 3] = lv2;
+    }
+#pragma unroll
+    for (int kb = NSS / 8; kb < 4; ++kb) {
+      aH[kb] = u32x4{0u, 0u, 0u, 0u};
+      aL[kb] = u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+
+  // S7 (model.py:128-136, :213-214) on the X waves: wave w candidates [16 (w - 4), +16) of the
+  // finished pass, lane (kq4, c) interests [16 kq4, 16 kq4 + 16), the 4 lane rows by permlanes
+  int pend_off = -1, pend_cnt = 0;
+  auto s7 = [&]() {
+    if (wave < 4) return;
+    const int lane = threadIdx.x & 63;
+    const int cl = lane & 15, kq4 = lane >> 4;
+    const int c = 16 * (wave & 3) + cl;
+    const float* F = reinterpret_cast<const float*>(smem + kWOffF);
+    float lg[16], m[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int o = c * 64 + ((16 * kq4 + j) ^ cl);
+      m[j] = F[o] * uc_pend;
+      if constexpr (WEIGHTED) lg[j] = F[4096 + o] * uc_pend;
+    }
+    float sc;
+    if constexpr (WEIGHTED) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) mx = fmaxf(mx, lg[j]);
+      mx = x_rows4_max(mx);
+      float sm = 0.f, num = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (16 * kq4 + j < KK) {
+          const float pe = x2_exp(lg[j] - mx);
+          sm += pe;
+          num = __builtin_fmaf(pe, m[j], num);
+        }
+      }
+      sm = x_rows4_sum(sm);
+      num = x_rows4_sum(num);
+      sc = num * __builtin_amdgcn_rcpf(sm);
+    } else {
+      if (p.score_type == MINER_SCORE_MAX) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) mx = fmaxf(mx, m[j]);
+        sc = x_rows4_max(mx);
+      } else {
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) sm += m[j];
+        sc = x_rows4_sum(sm) / (float)KK;
+      }
+    }
+    if (kq4 == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
+  };
+
+  f32x4 acc[4];
+  int t = 0;
+  // the products of one step in slot t & 1; NT candidate tiles compile-time (0: none)
+  auto compute_t = [&](int ci, int sg, bool mui_o, auto nt_c) {
+    constexpr int NT = decltype(nt_c)::value;
+    FRESH_LANE_IDS();
+    const int g = lane >> 4, i = lane & 15;
+    const char* slot = smem + (t & 1) * kWSlot;
+    const char* part = slot + P * kWPart;
+    f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb >= nkb) break;
+      u32x4 eH[2], eL[2];
+#pragma unroll
+      for (int ctl = 0; ctl < 2; ++ctl) {
+        const uint2 h0 = lds_tr(part + trH[ctl][0] + 4096 * kb), h1 = lds_tr(part + trH[ctl][1] + 4096 * kb);
+        const uint2 l0 = lds_tr(part + trL[ctl][0] + 4096 * kb), l1v = lds_tr(part + trL[ctl][1] + 4096 * kb);
+        eH[ctl] = u32x4{h0.x, h0.y, h1.x, h1.y};
+        eL[ctl] = u32x4{l0.x, l0.y, l1v.x, l1v.y};
+      }
+#pragma unroll
+      for (int ctl = 0; ctl < 2; ++ctl) hx[ctl] = mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
+    }
+    if (mui_o && 16 * kq + i < KK) {
+      const float mui_scale = __builtin_amdgcn_rcpf(kap);
+      float* dst = p.mui_out + ((size_t)imp_b(ci) * KK + 16 * kq + i) * d + 32 * sg + 4 * g;
+#pragma unroll
+      for (int ctl = 0; ctl < 2; ++ctl)
+        *reinterpret_cast<float4*>(dst + 16 * ctl) =
+            make_float4(hx[ctl][0] * mui_scale, hx[ctl][1] * mui_scale, hx[ctl][2] * mui_scale, hx[ctl][3] * mui_scale);
+    }
+    if constexpr (NT > 0) {
+      const char* cpart = slot + 2 * kWPart;
+      uint2 cH_[NT][2], cL_[NT][2];
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+#pragma unroll
+        for (int ctl = 0; ctl < 2; ++ctl) {
+          cH_[q][ctl] = lds_u64(cpart + cfH[ctl] + kWCTile * q);
+          cL_[q][ctl] = lds_u64(cpart + cfL[ctl] + kWCTile * q);
+        }
+      }
+      float x[8];
+      const float op_scale = P == 0 ? 1.0f / kSA : __builtin_amdgcn_rcpf(kap);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] = hx[0][e] * op_scale;
+        x[4 + e] = hx[1][e] * op_scale;
+      }
+      if (WEIGHTED && P == 1) {
+        gelu_as_pairs(x, 8);
+        const float sPj = kap * (1.0f / kSA);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] *= sPj;
+      }
+      u32x4 bH, bL;
+      split8h(x, bH, bL);
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const u32x4 ah = u32x4{cH_[q][0].x, cH_[q][0].y, cH_[q][1].x, cH_[q][1].y};
+        const u32x4 al = u32x4{cL_[q][0].x, cL_[q][0].y, cL_[q][1].x, cL_[q][1].y};
+        acc[q] = mfma_x2(acc[q], ah, al, bH, bL);
+      }
+    }
+  };
+  auto compute = [&](int ci, int sg, bool need_c, bool mui_o, int ntile) {
+    using std::integral_constant;
+    if (!need_c && !mui_o) return;
+    if (!need_c) compute_t(ci, sg, mui_o, integral_constant<int, 0>{});
+    else if (ntile >= 4) compute_t(ci, sg, mui_o, integral_constant<int, 4>{});
+    else if (ntile == 3) compute_t(ci, sg, mui_o, integral_constant<int, 3>{});
+    else if (ntile == 2) compute_t(ci, sg, mui_o, integral_constant<int, 2>{});
+    else compute_t(ci, sg, mui_o, integral_constant<int, 1>{});
+  };
+
+  // ---- prologue ----
+  for (int o = (int)threadIdx.x * 16; o < kWRing; o += kThreads * 16)      // rows no DMA writes read as 0
+    *reinterpret_cast<u32x4*>(smem + o) = u32x4{0u, 0u, 0u, 0u};
+  for (int o = (int)threadIdx.x * 16; o < kWLogB; o += kThreads * 16)      // stale logit rows stay finite
+    *reinterpret_cast<u32x4*>(smem + kWOffLog + o) = u32x4{0u, 0u, 0u, 0u};
+  for (int i = 0; i < 3; ++i) issue_L0(i);
+  vm_wait_all();
+  raw_barrier();
+  issue_L1(0); issue_L1(1);
+  vm_wait_all();
+  raw_barrier();
+  dedupe_prep(0);
+  raw_barrier();
+  dedupe_merge();
+  issue_L2(0);
+  vm_wait_all();
+  raw_barrier();
+  uint32_t cH[2], cC, nH[2] = {0u, 0u}, nC = 0u;
+  unsigned cLv = 0, nLv = 0;
+  item_offsets(0, 0, cH, cC, cLv);
+  dma_step(cH, cC, cLv, 0, 0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  for (int ci = 0; ci < n_i; ++ci) {
+    int c_off, c_cnt;
+    cands(ci, c_off, c_cnt);
+    const int cn = max(1, (c_cnt + 63) >> 6);
+    const int U = __builtin_amdgcn_readfirstlane(w_dup(ci)[0]);
+    nkb = (U + 31) >> 5;
+    for (int cp = 0; cp < cn; ++cp) {
+      const int cntp = min(64, c_cnt - 64 * cp);
+      const int ntile = (max(cntp, 1) + 15) >> 4;
+      const bool mui_o = P == 0 && p.mui_out != nullptr && cp == 0 && k_live;
+      const bool need_c = WITH_CAND && path_live && k_live;
+      const int ni = cp + 1 < cn ? ci : ci + 1, np = cp + 1 < cn ? cp + 1 : 0;
+      for (int sg = 0; sg < nst; ++sg, ++t) {
+        vm_wait_all();
+        raw_barrier();
+        if (cp == 0 && sg == 1) dedupe_merge();      // before this step's DMAs: the unit loads have landed
+        if (sg == 0) asm volatile("" : "+v"(uc_pend));  // the candidate units' load waited for here, not behind the DMAs
+        if (sg + 1 < nst) {
+          dma_step(cH, cC, cLv, sg + 1, (t + 1) & 1);
+        } else {
+          item_offsets(ni, np, nH, nC, nLv);
+          dma_step(nH, nC, nLv, 0, (t + 1) & 1);
+        }
+        if (sg == 0) {
+          if (WITH_CAND && pend_off >= 0) s7();
+          pend_off = -1;
+          if (cp == 0) {
+            using std::integral_constant;
+            if (nkb <= 2) softmax_w(ci, integral_constant<int, 16>{});
+            else softmax_w(ci, integral_constant<int, 32>{});
+            dedupe_prep(ci + 1);
+            issue_L0(ci + 3);
+            issue_L1(ci + 2);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else if (sg == 1 && cp == 0) {
+          issue_L2(ci + 1);                          // every wave has read impression ci's logit rows
+        }
+        compute(ci, sg, need_c, mui_o, ntile);
+      }
+      if (WITH_CAND && wave >= 4) {
+        const int c = 16 * (wave & 3) + (int)(threadIdx.x & 15);
+        const int id = w_cand(ci)[min(64 * cp + min(c, max(cntp, 1) - 1), kMaxCand - 1)];
+        uc_pend = p.unit_t[min(max(id, 0), p.n_news - 1)];
+      }
+      if constexpr (WITH_CAND) {
+        // pass done: the partial M / Lg of every wave -> F[P][c][k ^ (c & 15)] (S7 after the next barrier)
+        const int lane = threadIdx.x & 63;
+        const int j = lane & 15, g = lane >> 4;
+        if (path_live && k_live) {
+          const float pub_scale = kSA * __builtin_amdgcn_rcpf(kap);
+          float* F = reinterpret_cast<float*>(smem + kWOffF) + P * 4096;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (q < ntile) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int c = 16 * q + 4 * g + e;
+                F[c * 64 + ((16 * kq + j) ^ (c & 15))] = acc[q][e] * pub_scale;
+              }
+            }
+          }
+        }
+      }
+      pend_off = c_off + 64 * cp;
+      pend_cnt = cntp;
+      cH[0] = nH[0];
+      cH[1] = nH[1];
+      cC = nC;
+      cLv = nLv;
+    }
+  }
+  vm_wait_all();
+  raw_barrier();
+  if (WITH_CAND && pend_off >= 0) s7();
+}
+
+// ================================================================================================
 // host side
 // ================================================================================================
 int x2_num_cus() {
@@ -974,7 +1621,25 @@ int x2_num_cus() {
 
 inline bool al16(const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; }
 
+int x2w_launch(void* stream, const X2Params& prm) {
+  void (*kern)(X2Params) = nullptr;
+  const bool rg = prm.cand_off != nullptr;
+  switch (prm.score_type) {
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2w<MINER_SCORE_WEIGHTED, true> : news_score_x2w<MINER_SCORE_WEIGHTED, false>; break;
+    case MINER_SCORE_NONE: kern = news_score_x2w<MINER_SCORE_NONE, false>; break;
+    default: kern = rg ? news_score_x2w<MINER_SCORE_MAX, true> : news_score_x2w<MINER_SCORE_MAX, false>; break;
+  }
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+  if (e != hipSuccess) return (int)e;
+  int grid = x2_num_cus();
+  if (grid > prm.B) grid = prm.B;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), kWLds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
 int x2_launch(void* stream, const X2Params& prm) {
+  if (prm.L > kMaxL || prm.K > kMaxK) return x2w_launch(stream, prm);
   void (*kern)(X2Params) = nullptr;
   const bool rg = prm.cand_off != nullptr;
   if (prm.dis_out) {                   // eval with the eval loss (config/eval_miner.txt: metrics + loss)
@@ -1063,7 +1728,8 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
   if (!table2 || !table_unit || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
   if (L <= 0 || d <= 0 || K <= 0) return MINER_EINVAL;
-  if (L > kMaxL || K > kMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
+  if (L > kWMaxL || K > kWMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
+  if ((L > kMaxL || K > kMaxK) && disagree_out) return MINER_ESHAPE;   // the wide kernel writes mui instead
   if ((uint64_t)n_news * (uint64_t)d * 4u > 0xffffffffull) return MINER_ESHAPE;   // 32-bit row offsets
   if (score_type == MINER_SCORE_WEIGHTED && (!proj2 || !proj_unit)) return MINER_EINVAL;
   if (score_type != MINER_SCORE_NONE) {

@@ -107,7 +107,8 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
     total_samples = int(offs[-1]) if total_samples is None else total_samples
     L, d = beh.his_ids.shape[1], table.shape[1]
     max_c = 1 if category is not None else _max_candidates(offs, beh.n)
-    news_ok = news.supported(table.dtype, L, d, packed.Dc, packed.K)
+    news_ok = news.path_supported(table.dtype, L, d, packed.Dc, packed.K)
+    news_wide = news.wide_supported(table.dtype, L, d, packed.Dc, packed.K)   # K > 32 or L > 64 (news_score_x2w)
     if scorer == "news":
         if not news_ok:
             raise ValueError(f"scorer='news': the news path does not support L={L} d={d} K={packed.K}")
@@ -116,7 +117,7 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
     use_news = scorer == "news" or (scorer == "auto" and news_ok and max_c <= news.MAX_CAND)
     nt = news.precompute(table, packed, with_proj=score_type == "weighted") if use_news else None
     # fp32 pair-plane tables: the eval loss's disagreement is formed inside the scoring kernel (no mui)
-    fused_loss = want_loss and use_news and nt.x2 is not None and news.x2_enabled()
+    fused_loss = want_loss and use_news and nt.x2 is not None and news.x2_enabled() and not news_wide
     # with the per-candidate bias every candidate is one sample: chunk by samples (mui is [N, K, d])
     mc = max(_max_candidates(offs, beh.n), 1)
     step = chunk if category is None else max(1, chunk // mc)

@@ -30,6 +30,9 @@ from .ops import (PackedWeights, _as_packed, _contig, _dtype_code, _ptr, _requir
                   check_offsets)
 
 MAX_CAND = 512          # MINER_NEWS_MAX_CAND: candidates per impression
+X2W_MAX_L = 128         # MINER_NEWS_X2W_MAX_L: the fp32 pair-plane kernel's wide form (news_score_x2w)
+X2W_MAX_K = 64          # MINER_NEWS_X2W_MAX_K
+FUSED_MAX_K = 32        # the per-news precompute's packed Q (miner_pack_weights) holds K <= 32 rows
 
 
 @dataclasses.dataclass
@@ -67,6 +70,20 @@ class NewsTable:
 
 def supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int) -> bool:
     return _lib.lib().miner_news_supported(_dtype_code(dtype), L, d, Dc, K) == 0
+
+
+def wide_supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int) -> bool:
+    """Shapes past the news kernels' K <= 32 / L <= 64 that the fp32 pair-plane kernel scores in its
+    wide form (news_score_x2w: K <= 64, L <= 128, K % 4 == 0): fp32 tables with pair planes only
+    (not under MINER_NEWS_FP32=mfma32), no in-kernel disagreement (the eval loss uses mui)."""
+    return (dtype == torch.float32 and x2_enabled() and not supported(dtype, L, d, Dc, K)
+            and 0 < L <= X2W_MAX_L and 0 < K <= X2W_MAX_K and K % 4 == 0
+            and supported(dtype, 1, d, Dc, min(K, FUSED_MAX_K)))
+
+
+def path_supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int) -> bool:
+    """The news-id path takes (dtype, L, d, Dc, K): the news kernels or the wide pair-plane form."""
+    return supported(dtype, L, d, Dc, K) or wide_supported(dtype, L, d, Dc, K)
 
 
 def _check_shape(dt: int, L: int, d: int, Dc: int, K: int) -> None:
@@ -125,7 +142,15 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
     n_news, d = table.shape
     if pw.d != d:
         raise ValueError(f"packed weights are for d={pw.d}, the table has d={d}")
-    _check_shape(dt, 1, d, pw.Dc, pw.K)
+    wide_k = pw.K > FUSED_MAX_K
+    if wide_k:
+        # K > 32 (the wide pair-plane kernel): the logits in 32-interest slices of Q, each through the
+        # same precompute kernel (tanh(W1·e)·Q_sliceᵀ, exact fp32 per element as for K <= 32)
+        if not (0 < pw.K <= X2W_MAX_K and pw.K % 4 == 0) or pw.src is None or pw.src[0] is None:
+            raise ValueError(f"news path: K={pw.K} needs K <= {X2W_MAX_K}, K % 4 == 0 and the source weights")
+        _check_shape(dt, 1, d, pw.Dc, FUSED_MAX_K)
+    else:
+        _check_shape(dt, 1, d, pw.Dc, pw.K)
     if out is not None and out.table.data_ptr() == table.data_ptr() and tuple(out.logits.shape) == (n_news, pw.K) \
             and (out.proj is not None) == with_proj:
         logits, proj = out.logits, out.proj
@@ -133,8 +158,22 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
         logits = torch.empty((n_news, pw.K), device=table.device, dtype=torch.float32)
         proj = torch.empty((n_news, d), device=table.device, dtype=dtype) if with_proj else None
     with torch.cuda.device(table.device):
-        rc = _lib.lib().miner_news_precompute(_stream(table.device), dt, _ptr(table), n_news, _ptr(pw.buf), d,
-                                              pw.Dc, pw.K, _ptr(logits), _ptr(proj))
+        if not wide_k:
+            rc = _lib.lib().miner_news_precompute(_stream(table.device), dt, _ptr(table), n_news, _ptr(pw.buf), d,
+                                                  pw.Dc, pw.K, _ptr(logits), _ptr(proj))
+        else:
+            from .ops import pack_weights
+            w1, q, w2 = pw.src
+            for k0 in range(0, pw.K, FUSED_MAX_K):
+                k1 = min(k0 + FUSED_MAX_K, pw.K)
+                first = k0 == 0
+                part = pack_weights(w1, q[k0:k1], w2 if (first and with_proj) else None, dtype=dtype)
+                lg = torch.empty((n_news, k1 - k0), device=table.device, dtype=torch.float32)
+                rc = _lib.lib().miner_news_precompute(_stream(table.device), dt, _ptr(table), n_news, _ptr(part.buf),
+                                                      d, pw.Dc, k1 - k0, _ptr(lg), _ptr(proj) if first else None)
+                if rc != 0:
+                    break
+                logits[:, k0:k1].copy_(lg)
     _lib.check(rc, "miner_news_precompute")
     planes = None
     want_x2 = dtype == torch.float32 and (x2_enabled() if x2 is None else x2)
@@ -177,7 +216,16 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
     dt = _dtype_code(nt.dtype)
     B, L = his_ids.shape
     d, K = nt.d, nt.K
-    _check_shape(dt, L, d, 1, K)
+    wide = not supported(nt.dtype, L, d, 1, K)
+    if wide:
+        if not (nt.dtype == torch.float32 and 0 < L <= X2W_MAX_L and 0 < K <= X2W_MAX_K and K % 4 == 0):
+            _check_shape(dt, L, d, 1, K)
+        if nt.x2 is None or not (x2_enabled() if x2 is None else x2):
+            raise ValueError(f"news path: L={L} K={K} is past the news kernels (L <= 64, K <= 32); the wide "
+                             "form needs an fp32 table with pair planes (news.precompute(x2=True))")
+        if disagreement:
+            raise ValueError("disagreement=True: the wide form (L > 64 or K > 32) writes mui instead "
+                             "(return_user=True)")
     if st == _lib.SCORE_WEIGHTED and nt.proj is None:
         raise ValueError("score_type='weighted' needs the table precomputed with w_target (with_proj=True)")
     dev = nt.table.device

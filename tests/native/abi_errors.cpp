@@ -98,7 +98,9 @@ int main() {
   EXPECT(miner_news_split_x2(st, (const float*)mis, 10, 768, buf, fo), MINER_EALIGN);
   EXPECT(miner_score_news_x2(st, 9, buf, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 32, fo, nullptr, nullptr), MINER_EINVAL);
   EXPECT(miner_score_news_x2(st, 0, nullptr, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 32, fo, nullptr, nullptr), MINER_EINVAL);
-  EXPECT(miner_score_news_x2(st, 0, buf, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 65, 40, 768, 32, fo, nullptr, nullptr), MINER_ESHAPE);
+  EXPECT(miner_score_news_x2(st, 0, buf, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 129, 40, 768, 32, fo, nullptr, nullptr), MINER_ESHAPE);
+  EXPECT(miner_score_news_x2(st, 0, buf, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 68, fo, nullptr, nullptr), MINER_ESHAPE);
+  EXPECT(miner_score_news_x2(st, 0, buf, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 100, 40, 768, 64, fo, nullptr, fo), MINER_ESHAPE);
   EXPECT(miner_score_news_x2(st, 0, buf, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 30, fo, nullptr, nullptr), MINER_ESHAPE);
   EXPECT(miner_score_news_x2(st, 0, buf, fb, fb, nullptr, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 32, fo, nullptr, nullptr), MINER_EINVAL);
   EXPECT(miner_score_news_x2(st, 3, buf, fb, fb, buf, fb, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 32, nullptr, nullptr, nullptr), MINER_EINVAL);
