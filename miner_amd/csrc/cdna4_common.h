@@ -191,6 +191,9 @@ __device__ __forceinline__ float gelu_erfc_nr(float x) {
 // 1/16 of the bf16 rate: 2.67x the fp32 rate, and unlike the fp32 MFMA they co-issue with VALU.
 // ---------------------------------------------------------------------------------------------
 struct Split8 { u32x4 hi, mid, lo; };       // 8 fp32 elements as three bf16x8 operands
+#ifndef MINER_SPLIT3_INF
+#define MINER_SPLIT3_INF 2   // residual of a non-finite x: 0 none (inf - inf = NaN), 1 compare + select, 2 med3 clamp
+#endif
 
 __device__ __forceinline__ unsigned hi16_pack(unsigned a, unsigned b) {   // (a >> 16) | (b & 0xffff0000)
   return __builtin_amdgcn_perm(b, a, 0x07060302u);
@@ -198,9 +201,21 @@ __device__ __forceinline__ unsigned hi16_pack(unsigned a, unsigned b) {   // (a 
 __device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
   const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
   hi = hi16_pack(u0, u1);
+#if MINER_SPLIT3_INF == 1
   // an infinite x truncates to itself: its residual is 0, not inf - inf (a NaN x stays NaN in mid)
   const float h0 = __uint_as_float(u0 & 0xffff0000u), h1 = __uint_as_float(u1 & 0xffff0000u);
   const float r0 = x0 == h0 ? 0.f : x0 - h0, r1 = x1 == h1 ? 0.f : x1 - h1;
+#elif MINER_SPLIT3_INF == 2
+  // the residual of x clamped to the finite range (one v_med3 per element): an infinite x keeps hi =
+  // ±inf and finite mid / lo (FLT_MAX's low bits, absorbed by the infinite product), not the NaN of
+  // inf - inf; a NaN x stays NaN (med3 passes it through to r, and so to mid)
+  const float c0 = __builtin_amdgcn_fmed3f(x0, -3.40282347e38f, 3.40282347e38f);
+  const float c1 = __builtin_amdgcn_fmed3f(x1, -3.40282347e38f, 3.40282347e38f);
+  const float r0 = c0 - __uint_as_float(__float_as_uint(c0) & 0xffff0000u);
+  const float r1 = c1 - __uint_as_float(__float_as_uint(c1) & 0xffff0000u);
+#else
+  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+#endif
   const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
   mid = hi16_pack(v0, v1);
   const float q0 = r0 - __uint_as_float(v0 & 0xffff0000u), q1 = r1 - __uint_as_float(v1 & 0xffff0000u);

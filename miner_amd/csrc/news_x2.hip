@@ -1638,8 +1638,11 @@ int x2w_launch(void* stream, const X2Params& prm) {
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
+#ifndef X2_FORCE_WIDE
+#define X2_FORCE_WIDE 0   // A/B only: every shape through news_score_x2w
+#endif
 int x2_launch(void* stream, const X2Params& prm) {
-  if (prm.L > kMaxL || prm.K > kMaxK) return x2w_launch(stream, prm);
+  if (prm.L > kMaxL || prm.K > kMaxK || (X2_FORCE_WIDE && !prm.dis_out)) return x2w_launch(stream, prm);
   void (*kern)(X2Params) = nullptr;
   const bool rg = prm.cand_off != nullptr;
   if (prm.dis_out) {                   // eval with the eval loss (config/eval_miner.txt: metrics + loss)

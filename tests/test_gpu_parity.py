@@ -221,3 +221,33 @@ def test_x6_error_vs_fp32_mfma(scale, score_type, monkeypatch):
         assert ok, f"{form} at scale {scale} ({score_type}): off by {worst:.2f}x the tolerance"
     assert errs["x6"][0] <= 1.5 * errs["mfma32"][0] + 1e-7, errs
     assert errs["x6"][1] <= 1.5 * errs["mfma32"][1] + 1e-8 * rms, errs
+
+
+def test_x6_infinite_history_element(monkeypatch):
+    """An infinite element in a history row: the bf16x6 split of S1 (W1·Eᵀ) keeps hi =
+    ±inf with finite residuals (cdna4_common.h split3_pair), so tanh(W1·e) saturates as in the
+    reference instead of turning the impression NaN: mui equals the oracle's (torch fp32, the
+    reference op order) — ±inf exactly in the affected column, the fp32 bar everywhere else — and
+    the other impressions are untouched."""
+    monkeypatch.delenv("MINER_DENSE_FP32", raising=False)
+    g = torch.Generator().manual_seed(71)
+    B, L, C, d, Dc, K = 8, 20, 5, 256, 64, 16
+    E = torch.randn((B, L, d), generator=g) / d ** 0.5
+    cand = torch.randn((B, C, d), generator=g) / d ** 0.5
+    mask = torch.ones((B, L), dtype=torch.bool)
+    W1 = torch.randn((Dc, d), generator=g) * (2.0 / (Dc + d)) ** 0.5
+    Q = torch.randn((K, Dc), generator=g) * (2.0 / (K + Dc)) ** 0.5
+    W2 = torch.randn((d, d), generator=g) * (1.0 / d) ** 0.5
+    E[3, 7, 11] = float("inf")
+    E[5, 2, 100] = float("-inf")
+    s, mui = _ops().score(E.to(DEV), mask.to(DEV), cand.to(DEV), W1.to(DEV), Q.to(DEV), W2.to(DEV), return_user=True)
+    torch.cuda.synchronize()
+    ref_mui, ref = orc.score_torch(E, mask, cand, W1, Q, W2)
+    mui = mui.cpu()
+    assert torch.equal(torch.isnan(mui), torch.isnan(ref_mui)), "NaN pattern of mui differs from the reference"
+    assert torch.equal(torch.isinf(mui), torch.isinf(ref_mui)), "inf pattern of mui differs from the reference"
+    assert torch.equal(mui[torch.isinf(ref_mui)], ref_mui[torch.isinf(ref_mui)])
+    fin = torch.isfinite(ref_mui)
+    assert orc.parity_ok(mui[fin].numpy(), ref_mui[fin].numpy())[0]
+    ok_rows = [b for b in range(B) if b not in (3, 5)]
+    assert orc.parity_ok(s.cpu()[ok_rows].numpy(), ref[ok_rows].numpy())[0]

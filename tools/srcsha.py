@@ -11,6 +11,7 @@ KERNEL_SOURCES = {
     "news_x2": ("miner_amd/csrc/news_x2.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_news.h"),
     "news": ("miner_amd/csrc/news.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_news.h"),
     "miner_score": ("miner_amd/csrc/miner_score.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_score.h"),
+    "fastformer": ("miner_amd/csrc/fastformer.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_fastformer.h"),
 }
 
 
