@@ -91,7 +91,15 @@ int miner_score_news(void* stream, int dtype, int score_type, const void* news_t
  *   the eval loss's per-impression disagreement term, mean over k != k' of cos(mui_k, mui_k') with
  *   the diagonal zeroed (src/loss.py:81, src/utils.py:9-29), formed in the kernel from the Gram
  *   matrix of mui (no mui is written unless user_out is given).
+ *   Wide shapes (round 5): L up to MINER_NEWS_X2W_MAX_L and K up to MINER_NEWS_X2W_MAX_K (K % 4 ==
+ *   0) are scored by the kernel's wide form (news_score_x2w: 32-column steps, history groups in four
+ *   blocks of 32, four interest tiles); the reference limits neither (model.py:18-21, :159-185).
+ *   news_logits then has K columns: miner_news_precompute takes K <= 32, so a caller computes the
+ *   logits in 32-interest slices of Q (miner_pack_weights of each slice) and places them side by
+ *   side. disagree_out must be NULL there (the eval loss then reads user_out).
  */
+#define MINER_NEWS_X2W_MAX_L 128
+#define MINER_NEWS_X2W_MAX_K 64
 int miner_news_split_x2(void* stream, const float* src, int n, int d, void* dst, float* row_unit);
 int miner_score_news_x2(void* stream, int score_type, const void* table2, const float* table_unit,
                         const float* news_logits, const void* proj2, const float* proj_unit,

@@ -198,9 +198,20 @@ struct Split8 { u32x4 hi, mid, lo; };       // 8 fp32 elements as three bf16x8 o
 __device__ __forceinline__ unsigned hi16_pack(unsigned a, unsigned b) {   // (a >> 16) | (b & 0xffff0000)
   return __builtin_amdgcn_perm(b, a, 0x07060302u);
 }
+// SAFE: the operand may hold ±inf (activations: history rows, mui); the weight operands of the
+// dense kernel's S1 / S5 take the plain form (an infinite weight gives NaN in the reference too)
+template <bool SAFE = true>
 __device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
   const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
   hi = hi16_pack(u0, u1);
+  if constexpr (!SAFE) {
+    const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+    const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+    mid = hi16_pack(v0, v1);
+    const float q0 = r0 - __uint_as_float(v0 & 0xffff0000u), q1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+    lo = hi16_pack(__float_as_uint(q0), __float_as_uint(q1));
+    return;
+  }
 #if MINER_SPLIT3_INF == 1
   // an infinite x truncates to itself: its residual is 0, not inf - inf (a NaN x stays NaN in mid)
   const float h0 = __uint_as_float(u0 & 0xffff0000u), h1 = __uint_as_float(u1 & 0xffff0000u);
@@ -254,12 +265,13 @@ __device__ __forceinline__ f32x4 mma_x6(f32x4 c, const Split8& a, const Split8& 
 // of one slab product.
 // One 16-element step at a time (8 contraction elements per lane), so only 2 x 3 bf16 operand
 // registers quads are live beside the fp32 fragments.
+template <bool SAFE = true>
 __device__ __forceinline__ void split8_step(const Frag<float>& f, int st, u32x4& h, u32x4& m, u32x4& l) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {               // elements 8st + 2i, 8st + 2i + 1 -> dword i
     const int e = 8 * st + 2 * i;
     unsigned hh, mm, ll;
-    split3_pair(__uint_as_float(f.q[e >> 2][e & 3]), __uint_as_float(f.q[(e + 1) >> 2][(e + 1) & 3]), hh, mm, ll);
+    split3_pair<SAFE>(__uint_as_float(f.q[e >> 2][e & 3]), __uint_as_float(f.q[(e + 1) >> 2][(e + 1) & 3]), hh, mm, ll);
     h[i] = hh;
     m[i] = mm;
     l[i] = ll;
@@ -272,8 +284,9 @@ __device__ __forceinline__ void mma_slab_x6(f32x16& acc, const Frag<float>& a, c
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
     u32x4 ah, am, al, bh, bm, bl;
-    split8_step(a, st, ah, am, al);
-    split8_step(b, st, bh, bm, bl);
+    split8_step<false>(a, st, ah, am, al);     // the weights (S1 W1, S5 W2)
+    split8_step<true>(b, st, bh, bm, bl);      // the activations (E, mui): ±inf kept
+
     acc = mfma32_bf16(al, bh, acc);            // smallest terms first
     acc = mfma32_bf16(ah, bl, acc);
     acc = mfma32_bf16(am, bm, acc);

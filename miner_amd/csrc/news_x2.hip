@@ -1066,8 +1066,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 //     the dedupe of the next impression (wave 7); the logit rows of the next impression land in
 //     the single logit block at the second step.
 // The masked slots holding the first masked slot's news id form one group (as news_score_x2).
-constexpr int kWMaxL = 128;
-constexpr int kWMaxK = 64;
+constexpr int kWMaxL = MINER_NEWS_X2W_MAX_L;
+constexpr int kWMaxK = MINER_NEWS_X2W_MAX_K;
+static_assert(kWMaxL == 128 && kWMaxK == 64, "the wide carve below is laid out for L <= 128, K <= 64");
 constexpr int kWRB = 128;                              // bytes per staged row piece (32 hi | 32 lo)
 constexpr int kWPart = kWMaxL * kWRB;                  // 128 rows
 constexpr int kWCTile = 16 * kWRB + 16;                // candidate tiles 16 B apart (see kCTile)
