@@ -78,6 +78,9 @@ namespace {
 #ifndef X2_M0CLOB
 #define X2_M0CLOB 0    // A/B: the row DMAs leave M0 set (declared clobbered) instead of saving / restoring it
 #endif
+#ifndef X2_RING3
+#define X2_RING3 1     // the 3-slot ring for the MIND shape (MINER_X2_RING3=0 / 1 overrides at run time)
+#endif
 #ifndef X2_MERGE_EARLY
 #define X2_MERGE_EARLY 1 // the dedupe's unit merge right after a barrier, before the chunk's row DMAs are issued (its compiler wait then costs nothing)
 #endif
@@ -119,10 +122,55 @@ constexpr int kDupB = 16;
 constexpr int kX2Lds = kOffDup + 4 * kDupB;
 static_assert(kX2Lds <= 160 * 1024, "news_score_x2 LDS");
 
+// The carve as a function of the ring depth. R3 (X2_RING3, the MIND shape with dense candidates,
+// at most 48 per impression): three slots, two chunks in flight — history parts of 52 rows (<= 50
+// groups in 4-row DMA blocks; an MFMA block's reads past them land on the next part's finite rows,
+// times an attention weight 0), 3 candidate tiles, pass partials of 48 candidates, logit blocks of
+// 56 rows, no bias / Gram; the dedupe's row units and S7's candidate units come by LDS-DMA (no load
+// the compiler can see, so none of its vmcnt waits can drain the chunk in flight).
+template <bool R3> struct X2C {
+  static constexpr int kHisRows = R3 ? 52 : 64;
+  static constexpr int kCTiles = R3 ? 3 : 4;
+  static constexpr int kPart = kHisRows * kRB;
+  static constexpr int kCPart = kCTiles * kCTile;
+  static constexpr int kSlot = 2 * kPart + kCPart;
+  static constexpr int kNSlot = R3 ? 3 : 2;
+  static constexpr int kRing = kNSlot * kSlot;
+  static constexpr int kFBlk = (R3 ? 48 : 64) * 32;    // floats of one F[P][ch] block
+  static constexpr int kOffF = kRing;
+  static constexpr int kLogB = (R3 ? 56 : 64) * 128;
+  static constexpr int kOffLog = kOffF + 4 * kFBlk * 4;
+  static constexpr int kL1Cand = R3 ? 512 : 768;
+  static constexpr int kL1Unit = 768;                   // R3: the slots' E units | proj units
+  static constexpr int kL1B = R3 ? 768 + 512 : 4 * 64 * 3 + 4 * kMaxCand;
+  static constexpr int kOffL1 = kOffLog + 2 * kLogB;
+  static constexpr int kOffL0 = kOffL1 + 4 * kL1B;
+  static constexpr int kOffPrep = kOffL0 + 8 * kL0B;
+  static constexpr int kOffGram = kOffPrep + 3 * kPrepB;
+  static constexpr int kOffDup = kOffGram + (R3 ? 0 : kGramB);
+  static constexpr int kOffUc = kOffDup + 4 * kDupB;    // R3: S7's candidate units, 64 floats
+  static constexpr int kLds = kOffUc + (R3 ? 512 : 0);   // two buffers of 64
+};
+static_assert(X2C<false>::kLds == kX2Lds, "x2 carve");
+static_assert(X2C<true>::kLds <= 160 * 1024, "x2 R3 carve");
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// wait until at most n (wave-uniform, 0..7) of this wave's vector-memory operations are in flight
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+  }
+}
 
 __device__ __forceinline__ float x_both_max(float x) {
   const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -332,13 +380,14 @@ struct X2Params {
   int n_news, B, L, C, d, K, score_type;
 };
 
-__device__ __forceinline__ int* l1_his(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B); }
-__device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return reinterpret_cast<uint32_t*>(smem + kOffL1 + slot * kL1B + 256); }
-__device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + kOffL1 + slot * kL1B + 512); }
-__device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL1 + slot * kL1B + 768); }
-__device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffL0 + slot * kL0B); }
-__device__ __forceinline__ int* dup_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + kOffDup + slot * kDupB); }
-__device__ __forceinline__ float* prep_blk(char* smem, int i) { return reinterpret_cast<float*>(smem + kOffPrep + (i % 3) * kPrepB); }
+template <bool R3> __device__ __forceinline__ int* l1_his(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B); }
+template <bool R3> __device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return reinterpret_cast<uint32_t*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + 256); }
+template <bool R3> __device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + 512); }
+template <bool R3> __device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + X2C<R3>::kL1Cand); }
+template <bool R3> __device__ __forceinline__ float* l1_unit(char* smem, int slot) { return reinterpret_cast<float*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + X2C<R3>::kL1Unit); }
+template <bool R3> __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffL0 + slot * kL0B); }
+template <bool R3> __device__ __forceinline__ int* dup_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffDup + slot * kDupB); }
+template <bool R3> __device__ __forceinline__ float* prep_blk(char* smem, int i) { return reinterpret_cast<float*>(smem + X2C<R3>::kOffPrep + (i % 3) * kPrepB); }
 
 // NCH: 64-column chunks per row (0: d / 64 at run time). SHP 2: the MIND shape (history L = 50,
 // K = 32 interests) compile-time, no category bias and no mui output (plain scoring: the bench, the
@@ -348,7 +397,7 @@ __device__ __forceinline__ float* prep_blk(char* smem, int i) { return reinterpr
 // for both interest tiles (the transposed E reads are shared) and add the 3 Gram tiles of their 32
 // columns; at the pass end wave 2 hands its tiles to wave 0 through LDS, which forms D at the next
 // chunk (no mui is written).
-template <int ST, bool RAGGED, int NCH, int SHP, bool LOSS = false>
+template <int ST, bool RAGGED, int NCH, int SHP, bool LOSS = false, bool R3 = false>
 __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
@@ -365,7 +414,11 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // PIPE: impression ci's per-impression work runs spread over the chunks of pass 0 of impression
   // ci - 1 (schedule below), so no chunk carries all of it and the row stream keeps flowing; the
   // dedupe then moves to a mui wave (the X waves run S7)
-  constexpr bool PIPE = X2_PIPE && !LOSS && NCH >= 4;
+  using Cv = X2C<R3>;
+  static_assert(!R3 || (SHP == 2 && !RAGGED && !LOSS && NCH >= 2), "the 3-slot ring: MIND shape, dense, no eval loss");
+  // ring slot of chunk t (the kernel-wide chunk counter): t & 1, or t % 3 kept as a rotating index
+  auto slot_of = [&](int tt) { return R3 ? tt % 3 : (tt & 1); };
+  constexpr bool PIPE = X2_PIPE && !LOSS && NCH >= 4 && !R3;
   constexpr int kDedupeWave = PIPE ? 3 : X2_DEDUPE_WAVE;
   constexpr bool S7LATE = X2_S7_LATE && !PIPE && !LOSS && NCH >= 3;
   constexpr int cS7 = 1;                               // S7 of the previous pass (X waves), every pass
@@ -389,13 +442,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // the GELU (κ_k·2^-14), the pass-end factor of the M / Lg partials (2^14 / κ_k, leaving only the
   // candidate's unit for S7) and 1 / κ_k for the mui output. Set per impression.
   float kap = kSA;                         // κ_k of this lane's interest (the wave's path), per impression
-  float uc_pend = 1.0f;                    // S7 lane's candidate unit (X waves), loaded a chunk ahead
+  float uc_pend_r = 1.0f;                  // S7 lane's candidate unit (X waves), loaded a chunk ahead
+  int pend_ub = 0, pass_ctr = 0;           // R3: the candidate units' LDS buffer of the pending pass / this pass
 
   auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
   auto cands = [&](int i, int& off, int& cnt) {
     if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
     if constexpr (RAGGED) {
-      const int* o = l0_off(smem, i & 7);
+      const int* o = l0_off<R3>(smem, i & 7);
       off = __builtin_amdgcn_readfirstlane(o[0]);
       cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
     } else {
@@ -407,13 +461,13 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // ---- aux DMA jobs (after a barrier): L0 CSR offsets -> L1 ids / mask / bias -> L2 logit rows ----
   auto issue_L0 = [&](int i) {
     if (RAGGED && wave == 0 && i < n_i && (threadIdx.x & 63) < 2)
-      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kOffL0 + (i & 7) * kL0B);
+      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + Cv::kOffL0 + (i & 7) * kL0B);
   };
   auto issue_L1 = [&](int i) {
     if (i >= n_i) return;
     const int lane = threadIdx.x & 63;
     const size_t base = (size_t)imp_b(i) * L + min(lane, L - 1);
-    const unsigned l1 = sbase + kOffL1 + (i & 3) * kL1B;
+    const unsigned l1 = sbase + Cv::kOffL1 + (i & 3) * Cv::kL1B;
     if (wave == 1) {
       dma_b32(p.his_ids + base, l1);
     } else if (wave == 2) {
@@ -421,25 +475,25 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
       dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
     } else if (wave == 3) {
-      if (bias) dma_b32(bias + base, l1 + 512);
+      if (bias && !R3) dma_b32(bias + base, l1 + 512);
     } else if (WITH_CAND && wave >= 4) {                 // candidate ids, 64 per DMA
       int off, cnt;
       cands(i, off, cnt);
       for (int j = wave - 4; j >= 0 && 64 * j < cnt; j += 4) {
         const int c = min(64 * j + lane, cnt - 1);
-        dma_b32(p.cand_ids + off + c, l1 + 768 + 256 * j);
+        dma_b32(p.cand_ids + off + c, l1 + Cv::kL1Cand + 256 * j);
       }
     }
   };
   // logit rows of impression i by UNIQUE history row (after its dedupe, below)
   auto issue_L2 = [&](int i) {
-    if (i >= n_i) return;
+    if (i >= n_i || (R3 && wave == 7)) return;     // R3: 56 staged rows (<= 50 groups)
     const int lane = threadIdx.x & 63;
-    const int U = __builtin_amdgcn_readfirstlane(dup_u(smem, i & 3)[0]);
+    const int U = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, i & 3)[0]);
     const int row = min(8 * wave + (lane >> 3), U - 1);
     const int piece = min(lane & 7, (KK >> 2) - 1);
-    const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
-    x2_dma_b128(p.logits + (size_t)id * KK + 4 * piece, sbase + kOffLog + (i & 1) * kLogB + wave * 1024);
+    const int id = min(max(l1_his<R3>(smem, i & 3)[row], 0), p.n_news - 1);
+    x2_dma_b128(p.logits + (size_t)id * KK + 4 * piece, sbase + Cv::kOffLog + (i & 1) * Cv::kLogB + wave * 1024);
   };
   // The masked history slots holding the same news id — the left padding: every pad slot is the pad
   // news, masked (reader.py:101-110, :369) — form one group: its row is gathered and contracted once,
@@ -460,7 +514,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   auto dedupe_merge = [&]() {
     if (wave != kDedupeWave) return;
     if (du_i >= 0) {
-      int* pcp = reinterpret_cast<int*>(prep_blk(smem, du_i));
+      int* pcp = reinterpret_cast<int*>(prep_blk<R3>(smem, du_i));
+      if constexpr (R3) {
+        const int l = threadIdx.x & 63;
+        du_E = l1_unit<R3>(smem, du_i & 3)[l];
+        du_P = WEIGHTED ? l1_unit<R3>(smem, du_i & 3)[64 + l] : 1.0f;
+      }
       if (du_slot >= 0)
         pcp[du_slot] |= (((__float_as_int(du_E) >> 23) & 255) << 8) | (((__float_as_int(du_P) >> 23) & 255) << 16);
       du_i = -1;
@@ -471,16 +530,22 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int l = threadIdx.x & 63;
     dedupe_merge();
     if (i >= n_i) return;
-    int* his = l1_his(smem, i & 3);
+    int* his = l1_his<R3>(smem, i & 3);
     const int ls = min(l, L - 1);
     const int id = his[ls];
     const int idc = min(max(id, 0), p.n_news - 1);
-    du_E = p.unit_t[idc];
-    du_P = WEIGHTED ? p.unit_p[idc] : 1.0f;
-    const uint32_t mw = l1_mask(smem, i & 3)[ls];
+    if constexpr (R3) {                  // the units by LDS-DMA (read at the merge, an impression later)
+      const unsigned ub = sbase + (unsigned)((char*)l1_unit<R3>(smem, i & 3) - smem);
+      dma_b32(p.unit_t + idc, ub);
+      if (WEIGHTED) dma_b32(p.unit_p + idc, ub + 256);
+    } else {
+      du_E = p.unit_t[idc];
+      du_P = WEIGHTED ? p.unit_p[idc] : 1.0f;
+    }
+    const uint32_t mw = l1_mask<R3>(smem, i & 3)[ls];
     const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + ls) & 3);
     const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
-    const float bv = (keep && bias) ? l1_bias(smem, i & 3)[ls] : 0.f;
+    const float bv = (keep && bias) ? l1_bias<R3>(smem, i & 3)[ls] : 0.f;
     // the group: the masked slots holding the first masked slot's news id (a masked slot's logit and
     // bias never enter its score, model.py:176-180); every other slot is a group of its own
     const unsigned long long pads = __ballot(l < L && !keep);
@@ -492,7 +557,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const unsigned long long bal = __ballot(uniq);
     const int U = __popcll(bal);
     const int uidx = __popcll(bal & ((1ull << l) - 1ull));
-    float* pr = prep_blk(smem, i);
+    float* pr = prep_blk<R3>(smem, i);
     // (code, add) per group; code, an integer: bits 0-7 the multiplicity m, 8-15 / 16-23 the
     // exponent fields of the E / proj rows' units (powers of two; or'ed in by the next call), bit
     // 24 set for a click
@@ -506,7 +571,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       pc[l] = (113 << 8) | (113 << 16);  // m = 0, units 2^-14
       pr[64 + l] = -INFINITY;
     }
-    if (l == 0) dup_u(smem, i & 3)[0] = U;
+    if (l == 0) dup_u<R3>(smem, i & 3)[0] = U;
     du_slot = uniq ? uidx : -1;
     du_i = i;
   };
@@ -523,7 +588,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     int off = 0, cnt = 1;
     if (live) cands(i, off, cnt);
     const int cntp = max(1, min(64, cnt - 64 * pass));
-    const int U = live ? __builtin_amdgcn_readfirstlane(dup_u(smem, i & 3)[0]) : 1;
+    const int U = live ? __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, i & 3)[0]) : 1;
     lv = 0;
 #pragma unroll
     for (int jj = 0; jj < kNB; ++jj) {
@@ -534,8 +599,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       const uint32_t poff = (uint32_t)(((lane & 15) ^ x2swz(row)) << 4);
       int h = 0, c = 0;
       if (live) {
-        if (dmaE || dmaP) h = l1_his(smem, i & 3)[min(row, U - 1)];
-        if (dmaC) c = l1_cand(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
+        if (dmaE || dmaP) h = l1_his<R3>(smem, i & 3)[min(row, U - 1)];
+        if (dmaC) c = l1_cand<R3>(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
       }
       h = min(max(h, 0), p.n_news - 1);
       c = min(max(c, 0), p.n_news - 1);
@@ -545,19 +610,26 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     }
     lv = __builtin_amdgcn_readfirstlane(lv);
   };
-  auto dma_chunk = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int cc, int slot) {
-    if (lv == 0 || (X2_ABL & 2)) return;
+  // returns the number of row DMAs this wave issued (wave-uniform): the ring-3 wait keeps them in flight
+  auto dma_chunk = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int cc, int slot) -> int {
+    if (lv == 0 || (X2_ABL & 2)) return 0;
+    int n = 0;
     const char* bE = tabB + cc * kRB;
     const char* bP = prjB + cc * kRB;
 #pragma unroll
     for (int jj = 0; jj < kNB; ++jj) {
-      const unsigned m = sbase + slot * kSlot + dma_block(jj) * 1024;
+      const unsigned m = sbase + slot * Cv::kSlot + dma_block(jj) * 1024;
       if (lv & (1u << jj)) {
         if (dmaE) x2_dma_row(oH[jj], bE, m);
-        if (dmaP) x2_dma_row(oH[jj], bP, m + kPart);
+        if (dmaP) x2_dma_row(oH[jj], bP, m + Cv::kPart);
+        n += (dmaE ? 1 : 0) + (dmaP ? 1 : 0);
       }
-      if (lv & (16u << jj)) x2_dma_row(oC[jj], bE, m + 2 * kPart + (dma_block(jj) >> 2) * 16);
+      if (lv & (16u << jj)) {
+        x2_dma_row(oC[jj], bE, m + 2 * Cv::kPart + (dma_block(jj) >> 2) * 16);
+        ++n;
+      }
     }
+    return n;
   };
 
   // ---- per-lane LDS read offsets (fixed for the launch) ----
@@ -600,8 +672,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const int k = 16 * ktile + j;
-    const float* lgb = reinterpret_cast<const float*>(smem + kOffLog + (i & 1) * kLogB);
-    const float* pr = prep_blk(smem, i);
+    const float* lgb = reinterpret_cast<const float*>(smem + Cv::kOffLog + (i & 1) * Cv::kLogB);
+    const float* pr = prep_blk<R3>(smem, i);
     const int* pc = reinterpret_cast<const int*>(pr);
     const unsigned sh = pth ? 16u : 8u;
     float v[NSS], wm[NSS], un[NSS];
@@ -644,7 +716,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   };
 
   // ring rows no DMA writes read as zeros; the prologue's first barrier orders these stores first
-  for (int o = (int)threadIdx.x * 16; o < kRingB; o += kThreads * 16)
+  for (int o = (int)threadIdx.x * 16; o < Cv::kRing; o += kThreads * 16)
     *reinterpret_cast<u32x4*>(smem + o) = u32x4{0u, 0u, 0u, 0u};
   for (int i = 0; i < 4; ++i) issue_L0(i);
   vm_wait_all();
@@ -652,7 +724,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   issue_L1(0); issue_L1(1); issue_L1(2);
   vm_wait_all();
   raw_barrier();
-  dedupe_prep(0); dedupe_prep(1);
+  dedupe_prep(0);
+  if (R3) vm_wait_all();               // impression 0's units (LDS-DMA) landed before dedupe_prep(1) merges them
+  dedupe_prep(1);
   raw_barrier();
   issue_L2(0); issue_L2(1);
   vm_wait_all();
@@ -663,6 +737,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   unsigned cLv = 0, nLv = 0;
   item_offsets(0, 0, cH, cC, cLv);
   dma_chunk(cH, cC, cLv, 0, 0);
+  int n_ahead = 0;                               // R3: row DMAs of the chunk one ahead, still in flight
+  if constexpr (R3) n_ahead = dma_chunk(cH, cC, cLv, 1, 1);
 
   f32x4 acc[4];                                  // this wave's M / Lg partials, candidate tiles 0..3
 #pragma unroll
@@ -682,8 +758,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   auto form_d = [&](int b) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
-    const float* pg = reinterpret_cast<const float*>(smem + kOffGram);
-    float* nrm = reinterpret_cast<float*>(smem + kOffGram + 3 * 256 * 4);
+    const float* pg = reinterpret_cast<const float*>(smem + Cv::kOffGram);
+    float* nrm = reinterpret_cast<float*>(smem + Cv::kOffGram + 3 * 256 * 4);
 #pragma unroll
     for (int q = 0; q < 3; ++q)
 #pragma unroll
@@ -715,18 +791,19 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // finished pass, lane (kq, c) interests [8 kq, 8 kq + 8); the two column-half partials summed
   // here (ch 0 + ch 1), the 4 lane rows combined by permlanes
   auto s7 = [&]() {
-    if (wave < 4) return;
+    if (wave < 4 || (R3 && wave == 7)) return;          // R3: <= 48 candidates, waves 4-6
     const int lane = threadIdx.x & 63;
     const int cl = lane & 15, kq = lane >> 4;
     const int c = 16 * (wave & 3) + cl;
-    const float* F = reinterpret_cast<const float*>(smem + kOffF);
+    const float* F = reinterpret_cast<const float*>(smem + Cv::kOffF);
+    const float uc_pend = R3 ? reinterpret_cast<const float*>(smem + Cv::kOffUc)[64 * pend_ub + c] : uc_pend_r;
     const int sw = (c >> 1) & 31;
     float lg[8], m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int o = c * 32 + ((8 * kq + j) ^ sw);
-      m[j] = (F[o] + F[2048 + o]) * uc_pend;                        // the candidate row's unit
-      if constexpr (WEIGHTED) lg[j] = (F[4096 + o] + F[6144 + o]) * uc_pend;
+      m[j] = (F[o] + F[Cv::kFBlk + o]) * uc_pend;                   // the candidate row's unit
+      if constexpr (WEIGHTED) lg[j] = (F[2 * Cv::kFBlk + o] + F[3 * Cv::kFBlk + o]) * uc_pend;
     }
     float sc;
     if constexpr (WEIGHTED) {
@@ -769,8 +846,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     constexpr int NT = decltype(nt_c)::value;
     FRESH_LANE_IDS();
     const int g = lane >> 4, i = lane & 15;
-    const char* slot = smem + (t & 1) * kSlot;
-    const char* part = slot + P * kPart;
+    const char* slot = smem + slot_of(t) * Cv::kSlot;
+    const char* part = slot + P * Cv::kPart;
     f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     [[maybe_unused]] f32x4 hy[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -825,7 +902,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       // reads of tiles q and q + 1 are not paired into a ds_read2st64_b64, whose 16-lane groups bank
       // by dword mod 32 — a 2-way conflict on these 16-row reads (MI355X_MICROARCH.md §LDS) —
       // while ds_read_b64 banks mod 64 over 32 lanes: none
-      const char* cpart = slot + 2 * kPart;
+      const char* cpart = slot + 2 * Cv::kPart;
       uint2 cH_[NT][2], cL_[NT][2];
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
@@ -876,7 +953,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   if constexpr (PIPE) {                          // impression 0's attention weights (the rest: a chunk schedule ahead)
     using std::integral_constant;
     if (n_i > 0) {
-      const int nkb0 = __builtin_amdgcn_readfirstlane(dup_u(smem, 0)[0]) > 32 ? 2 : 1;
+      const int nkb0 = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, 0)[0]) > 32 ? 2 : 1;
       if (X2_SOFT_HALF && nkb0 == 1) softmax_inwave(0, kt, P, aH, aL, kap, integral_constant<int, 8>{});
       else softmax_inwave(0, kt, P, aH, aL, kap, integral_constant<int, 16>{});
     }
@@ -887,7 +964,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     int c_off, c_cnt;
     cands(ci, c_off, c_cnt);
     const int cn = max(1, (c_cnt + 63) >> 6);
-    nkb = __builtin_amdgcn_readfirstlane(dup_u(smem, ci & 3)[0]) > 32 ? 2 : 1;
+    nkb = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, ci & 3)[0]) > 32 ? 2 : 1;
     for (int cp = 0; cp < cn; ++cp) {
       const int cntp = min(64, c_cnt - 64 * cp);
       const int ntile = (max(cntp, 1) + 15) >> 4;
@@ -900,12 +977,23 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       bool did_s7 = false;
       for (int cc = 0; cc < nchunk; ++cc, ++t) {
         X2_STAMP(7);
-        vm_wait_all();                 // this chunk's rows (and every older DMA) landed for this wave,
+        // this chunk's rows (and every older DMA) landed for this wave (R3: the next chunk's stay in
+        // flight — they are the n_ahead youngest, or younger operations force part of them), then
+        // for every wave; the slot of the last chunk is free
+        if constexpr (R3) vm_wait_n(n_ahead);
+        else vm_wait_all();
         X2_STAMP(0);
-        raw_barrier();                 // then for every wave; the other slot is free
+        raw_barrier();
         X2_STAMP(1);
         auto issue_next = [&]() {
-          if (cc + 1 < nchunk) {
+          if constexpr (R3) {          // two chunks ahead, into the slot chunk cc - 1 just left
+            if (cc + 2 < nchunk) {
+              n_ahead = dma_chunk(cH, cC, cLv, cc + 2, slot_of(t + 2));
+            } else {
+              if (cc + 2 == nchunk) item_offsets(ni, np, nH, nC, nLv);
+              n_ahead = dma_chunk(nH, nC, nLv, cc + 2 - nchunk, slot_of(t + 2));
+            }
+          } else if (cc + 1 < nchunk) {
             dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
           } else {
             item_offsets(ni, np, nH, nC, nLv);
@@ -942,7 +1030,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
             if (cc == cL2) issue_L2(ci + 2);   // into the block impression ci's logits were read from
             if (((cc == cSM0 && P == 0) || (cc == cSM1 && P == 1)) && ci + 1 < n_i) {
               using std::integral_constant;
-              nkb_n = __builtin_amdgcn_readfirstlane(dup_u(smem, (ci + 1) & 3)[0]) > 32 ? 2 : 1;
+              nkb_n = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, (ci + 1) & 3)[0]) > 32 ? 2 : 1;
               if (X2_SOFT_HALF && nkb_n == 1) softmax_inwave(ci + 1, kt, P, aHn, aLn, kapn, integral_constant<int, 8>{});
               else softmax_inwave(ci + 1, kt, P, aHn, aLn, kapn, integral_constant<int, 16>{});
             }
@@ -952,6 +1040,11 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           if (!S7LATE) {
             if (WITH_CAND && pend_off >= 0) s7();
             pend_off = -1;
+          }
+          if (R3 && WITH_CAND && wave == 4) {   // this pass's candidate units -> LDS (read by its S7, a pass later)
+            const int lane = threadIdx.x & 63;
+            const int id = l1_cand<R3>(smem, ci & 3)[min(64 * cp + min(lane, max(cntp, 1) - 1), kMaxCand - 1)];
+            dma_b32(p.unit_t + min(max(id, 0), p.n_news - 1), sbase + Cv::kOffUc + (pass_ctr & 1) * 256);
           }
           if (LOSS && pend_d >= 0) form_d(pend_d);
           pend_d = -1;
@@ -987,18 +1080,20 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         X2_STAMP(3);
         compute(ci, cc, mode, ntile);
       }
-      if (WITH_CAND && wave >= 4) {
+      if (!R3 && WITH_CAND && wave >= 4) {
         // this pass's S7 (after the next barrier) needs its candidates' row units: one per lane
         const int c = 16 * (wave & 3) + (int)(threadIdx.x & 15);
-        const int id = l1_cand(smem, ci & 3)[min(64 * cp + min(c, max(cntp, 1) - 1), kMaxCand - 1)];
-        uc_pend = p.unit_t[min(max(id, 0), p.n_news - 1)];
+        const int id = l1_cand<R3>(smem, ci & 3)[min(64 * cp + min(c, max(cntp, 1) - 1), kMaxCand - 1)];
+        uc_pend_r = p.unit_t[min(max(id, 0), p.n_news - 1)];
       }
+      pend_ub = pass_ctr & 1;
+      ++pass_ctr;
       if (nchunk == 1 && did_s7) raw_barrier();
       if (LOSS && dis_out && cp == 0) {
         // the Gram hand-off: wave 2 (columns 32..63 of each chunk) -> LDS -> wave 0 at the next chunk
         if (gram_w && ch == 1) {
           const int lane = threadIdx.x & 63;
-          float* pg = reinterpret_cast<float*>(smem + kOffGram);
+          float* pg = reinterpret_cast<float*>(smem + Cv::kOffGram);
 #pragma unroll
           for (int q = 0; q < 3; ++q)
 #pragma unroll
@@ -1018,7 +1113,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         if (path_live && k_live) {
           // in true units over the candidate row's unit: M = M_s·unit_c·2^14/κ_k (Lg likewise)
           const float pub_scale = kSA * __builtin_amdgcn_rcpf(kap);
-          float* F = reinterpret_cast<float*>(smem + kOffF) + (P * 2 + ch) * 2048;
+          float* F = reinterpret_cast<float*>(smem + Cv::kOffF) + (P * 2 + ch) * Cv::kFBlk;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (q < ntile) {
@@ -1645,6 +1740,7 @@ int x2w_launch(void* stream, const X2Params& prm) {
 int x2_launch(void* stream, const X2Params& prm) {
   if (prm.L > kMaxL || prm.K > kMaxK || (X2_FORCE_WIDE && !prm.dis_out)) return x2w_launch(stream, prm);
   void (*kern)(X2Params) = nullptr;
+  int lds = kX2Lds;
   const bool rg = prm.cand_off != nullptr;
   if (prm.dis_out) {                   // eval with the eval loss (config/eval_miner.txt: metrics + loss)
 #define X2_PICKL(NCHV)                                                                                       \
@@ -1675,22 +1771,27 @@ int x2_launch(void* stream, const X2Params& prm) {
   }
   const bool plain = prm.L == 50 && prm.K == 32 && !prm.bias && !prm.mui_out && prm.score_type == MINER_SCORE_WEIGHTED &&
                      !getenv("MINER_NEWS_SHP_RT");
+  // the 3-slot ring (two chunks in flight): the MIND shape with dense candidates, at most 48 of them
+  const char* r3e = getenv("MINER_X2_RING3");
+  const bool ring3 = plain && !rg && prm.C <= 48 && (r3e ? r3e[0] == '1' : X2_RING3 != 0);
   if (prm.d == 768) {                  // config 3 (MIND-large): the chunk count compile-time
-    if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 12, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2>;
+    if (ring3) { kern = news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2, false, true>; lds = X2C<true>::kLds; }
+    else if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 12, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2>;
     else { X2_PICK(12) }
   } else if (prm.d == 256) {           // config 2 (MIND-small)
-    if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 4, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2>;
+    if (ring3) { kern = news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2, false, true>; lds = X2C<true>::kLds; }
+    else if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 4, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2>;
     else { X2_PICK(4) }
   } else {
     X2_PICK(0)
   }
   }
 #undef X2_PICK
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kX2Lds);
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   int grid = x2_num_cus();
   if (grid > prm.B) grid = prm.B;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), kX2Lds, static_cast<hipStream_t>(stream), prm);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, static_cast<hipStream_t>(stream), prm);
   e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;
 }

@@ -334,6 +334,26 @@ def test_masked_slot_groups(dtype, monkeypatch):
     _ok(s_plain, ref_plain, dtype, "plain scores")
 
 
+@pytest.mark.parametrize("d,C", [(768, 40), (768, 48), (256, 40), (768, 33)])
+def test_x2_ring3_equals_ring2(d, C, monkeypatch):
+    """The 3-slot ring (two chunks in flight; the MIND shape L = 50, K = 32, plain scoring, dense
+    candidates, C <= 48) gives the 2-slot kernel's scores bit for bit, and the oracle's at the fp32
+    bar; padded and full histories, several impressions per workgroup."""
+    monkeypatch.setenv("MINER_NEWS_FP32", "x2")
+    B = 1200
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(40 + C, B, 50, d, 4000, torch.float32, C=C)
+    mask[:100] = True                                    # full histories: 50 groups, both blocks
+    nt = news.precompute(table, W1, Q, W2)
+    monkeypatch.setenv("MINER_X2_RING3", "1")
+    s3 = news.score(nt, hid, mask, cid)
+    monkeypatch.setenv("MINER_X2_RING3", "0")
+    s2 = news.score(nt, hid, mask, cid)
+    torch.cuda.synchronize()
+    assert torch.equal(s3, s2), float((s3 - s2).abs().max())
+    _, ref = _oracle(table, hid, mask, cid, None, W1, Q, W2)
+    _ok(s3, ref, torch.float32, "ring-3 scores")
+
+
 def test_x2_nan_logit_propagates(monkeypatch):
     """A NaN in a clicked slot's logit (here through the category bias) makes the reference's softmax
     over the history NaN for that impression (torch softmax propagates it, model.py:176-181), so every
