@@ -79,7 +79,7 @@ namespace {
 #define X2_M0CLOB 0    // A/B: the row DMAs leave M0 set (declared clobbered) instead of saving / restoring it
 #endif
 #ifndef X2_RING3
-#define X2_RING3 1     // the 3-slot ring for the MIND shape (MINER_X2_RING3=0 / 1 overrides at run time)
+#define X2_RING3 0     // (measured +5.4 %, r05) the 3-slot ring for the MIND shape (MINER_X2_RING3=0 / 1 overrides at run time)
 #endif
 #ifndef X2_MERGE_EARLY
 #define X2_MERGE_EARLY 1 // the dedupe's unit merge right after a barrier, before the chunk's row DMAs are issued (its compiler wait then costs nothing)
@@ -1161,26 +1161,36 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 //     the dedupe of the next impression (wave 7); the logit rows of the next impression land in
 //     the single logit block at the second step.
 // The masked slots holding the first masked slot's news id form one group (as news_score_x2).
-constexpr int kWMaxL = MINER_NEWS_X2W_MAX_L;
-constexpr int kWMaxK = MINER_NEWS_X2W_MAX_K;
-static_assert(kWMaxL == 128 && kWMaxK == 64, "the wide carve below is laid out for L <= 128, K <= 64");
 constexpr int kWRB = 128;                              // bytes per staged row piece (32 hi | 32 lo)
-constexpr int kWPart = kWMaxL * kWRB;                  // 128 rows
 constexpr int kWCTile = 16 * kWRB + 16;                // candidate tiles 16 B apart (see kCTile)
-constexpr int kWSlot = 2 * kWPart + 4 * kWCTile;
-constexpr int kWRing = 2 * kWSlot;
-constexpr int kWOffF = kWRing;                         // F[P] [c 64][k ^ (c & 15)] fp32
-constexpr int kWFB = 2 * 64 * 64 * 4;
-constexpr int kWOffLog = kWOffF + kWFB;                // logit rows of one impression [group][64]
-constexpr int kWLogB = kWMaxL * kWMaxK * 4;
-constexpr int kWOffL1 = kWOffLog + kWLogB;             // 3 slots: his ids | mask words | bias | cand ids
-constexpr int kWL1B = 3 * 4 * kWMaxL + 4 * kMaxCand;
-constexpr int kWOffL0 = kWOffL1 + 3 * kWL1B;           // 8 slots: CSR offsets (ragged)
-constexpr int kWOffPrep = kWOffL0 + 8 * kL0B;          // 2 blocks: code[128] | add[128]
-constexpr int kWPrepB = 2 * kWMaxL * 4;
-constexpr int kWOffDup = kWOffPrep + 2 * kWPrepB;      // per L1 slot: U
-constexpr int kWLds = kWOffDup + 3 * kDupB;
-static_assert(kWLds <= 160 * 1024, "news_score_x2w LDS");
+// The carve by workgroup size. NW = 8: the wide form (K <= 64, L <= 128, one workgroup per CU).
+// NW = 4 (A/B, MINER_X2_W4): K <= 32, L <= 64, dense C <= 256, in 80 KB, two workgroups per CU —
+// each with its own barriers, so one workgroup's per-impression work runs beside the other's stream.
+template <int NW> struct XW {
+  static constexpr int kThr = 64 * NW;
+  static constexpr int kMaxL = NW == 8 ? MINER_NEWS_X2W_MAX_L : 64;
+  static constexpr int kMaxK = NW == 8 ? MINER_NEWS_X2W_MAX_K : 32;
+  static constexpr int kMaxC = NW == 8 ? kMaxCand : 256;
+  static constexpr int kNKb = kMaxL / 32;                // history blocks of 32 groups
+  static constexpr int kHalves = kMaxL / 64;             // 64-slot ballots of the dedupe
+  static constexpr int kPart = kMaxL * kWRB;
+  static constexpr int kSlot = 2 * kPart + 4 * kWCTile;
+  static constexpr int kRing = 2 * kSlot;
+  static constexpr int kOffF = kRing;                    // F[P] [c 64][k ^ (c & 15)] fp32
+  static constexpr int kFP = 64 * kMaxK;                 // floats per path
+  static constexpr int kOffLog = kOffF + 2 * kFP * 4;    // logit rows of one impression [group][kMaxK]
+  static constexpr int kLogB = kMaxL * kMaxK * 4;
+  static constexpr int kOffL1 = kOffLog + kLogB;         // 3 slots: his ids | mask words | bias | cand ids
+  static constexpr int kL1B = 3 * 4 * kMaxL + 4 * kMaxC;
+  static constexpr int kOffL0 = kOffL1 + 3 * kL1B;       // 8 slots: CSR offsets (ragged)
+  static constexpr int kOffPrep = kOffL0 + 8 * kL0B;     // 2 blocks: code[kMaxL] | add[kMaxL]
+  static constexpr int kPrepB = 2 * kMaxL * 4;
+  static constexpr int kOffDup = kOffPrep + 2 * kPrepB;  // per L1 slot: U
+  static constexpr int kLds = kOffDup + 3 * kDupB;
+};
+static_assert(XW<8>::kMaxL == 128 && XW<8>::kMaxK == 64, "the wide carve is laid out for L <= 128, K <= 64");
+static_assert(XW<8>::kLds <= 160 * 1024, "news_score_x2w LDS");
+static_assert(XW<4>::kLds <= 80 * 1024, "news_score_x2w<4>: two workgroups per CU");
 
 // 16-byte chunk swizzle of a staged 128-byte row (8 chunks: hi 0..3, lo 4..7): slot = chunk ^
 // wswz(row). Over the 4 same-parity rows of a transposed read's 8-row group it takes the even
@@ -1189,8 +1199,9 @@ static_assert(kWLds <= 160 * 1024, "news_score_x2w LDS");
 // all 8 values: both reads are conflict-free (ds_read_b64 / _tr_b16 bank over 256 B per 32 lanes)
 __host__ __device__ inline int wswz(int row) { return (((row >> 1) & 3) << 1) | ((row >> 3) & 1); }
 
-template <int ST, bool RAGGED>
-__global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
+template <int ST, bool RAGGED, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 2) void news_score_x2w(X2Params p) {
+  using Cw = XW<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
   constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
@@ -1199,39 +1210,39 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
   const int L = p.L, KK = p.K, d = p.d;
   const int nst = d >> 5;                                 // 32-column steps
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int P = wave >> 2, kq = wave & 3;
+  const int P = wave / (NW / 2), kq = wave % (NW / 2);   // path, interest tile
   const bool k_live = 16 * kq < KK;
   const bool path_live = P == 0 || WEIGHTED;
   const char* tabB = static_cast<const char*>(p.table2);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj2) : tabB;
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
   float kap = kSA;                         // κ_k of this lane's interest (the wave's path), per impression
-  float uc_pend = 1.0f;                    // S7 lane's candidate unit (X waves)
+  float uc_pend[8 / NW] = {};              // S7 lane's candidate units (X waves), one per round
 
   auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
-  auto l1 = [&](int i) { return smem + kWOffL1 + (i % 3) * kWL1B; };
+  auto l1 = [&](int i) { return smem + Cw::kOffL1 + (i % 3) * Cw::kL1B; };
   auto w_his = [&](int i) { return reinterpret_cast<int*>(l1(i)); };
-  auto w_mask = [&](int i) { return reinterpret_cast<uint32_t*>(l1(i) + 4 * kWMaxL); };
-  auto w_bias = [&](int i) { return reinterpret_cast<float*>(l1(i) + 8 * kWMaxL); };
-  auto w_cand = [&](int i) { return reinterpret_cast<int*>(l1(i) + 12 * kWMaxL); };
-  auto w_dup = [&](int i) { return reinterpret_cast<int*>(smem + kWOffDup + (i % 3) * kDupB); };
-  auto w_prep = [&](int i) { return reinterpret_cast<float*>(smem + kWOffPrep + (i & 1) * kWPrepB); };
+  auto w_mask = [&](int i) { return reinterpret_cast<uint32_t*>(l1(i) + 4 * Cw::kMaxL); };
+  auto w_bias = [&](int i) { return reinterpret_cast<float*>(l1(i) + 8 * Cw::kMaxL); };
+  auto w_cand = [&](int i) { return reinterpret_cast<int*>(l1(i) + 12 * Cw::kMaxL); };
+  auto w_dup = [&](int i) { return reinterpret_cast<int*>(smem + Cw::kOffDup + (i % 3) * kDupB); };
+  auto w_prep = [&](int i) { return reinterpret_cast<float*>(smem + Cw::kOffPrep + (i & 1) * Cw::kPrepB); };
   auto cands = [&](int i, int& off, int& cnt) {
     if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
     if constexpr (RAGGED) {
-      const int* o = reinterpret_cast<const int*>(smem + kWOffL0 + (i & 7) * kL0B);
+      const int* o = reinterpret_cast<const int*>(smem + Cw::kOffL0 + (i & 7) * kL0B);
       off = __builtin_amdgcn_readfirstlane(o[0]);
       cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
     } else {
       off = imp_b(i) * p.C;
       cnt = p.C;
     }
-    cnt = min(max(cnt, 0), kMaxCand);
+    cnt = min(max(cnt, 0), Cw::kMaxC);
   };
   // ---- aux DMAs: L0 CSR offsets -> L1 ids / mask / bias / candidate ids -> L2 logit rows by group ----
   auto issue_L0 = [&](int i) {
     if (RAGGED && wave == 0 && i < n_i && (threadIdx.x & 63) < 2)
-      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + kWOffL0 + (i & 7) * kL0B);
+      dma_b32(p.cand_off + imp_b(i) + (threadIdx.x & 63), sbase + Cw::kOffL0 + (i & 7) * kL0B);
   };
   auto issue_L1 = [&](int i) {
     if (i >= n_i) return;
@@ -1243,17 +1254,17 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
         dma_b32(p.his_ids + base, dst + 256 * hh);
       } else if (wave == 2) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
-        dma_b32(reinterpret_cast<const void*>(a), dst + 4 * kWMaxL + 256 * hh);
+        dma_b32(reinterpret_cast<const void*>(a), dst + 4 * Cw::kMaxL + 256 * hh);
       } else if (wave == 3) {
-        if (p.bias) dma_b32(p.bias + base, dst + 8 * kWMaxL + 256 * hh);
+        if (p.bias) dma_b32(p.bias + base, dst + 8 * Cw::kMaxL + 256 * hh);
       }
     }
-    if (WITH_CAND && wave >= 4) {
+    if (WITH_CAND && (NW == 8 ? wave >= 4 : wave == 0)) {   // candidate ids, 64 per DMA
       int off, cnt;
       cands(i, off, cnt);
-      for (int j = wave - 4; 64 * j < cnt; j += 4) {
+      for (int j = NW == 8 ? wave - 4 : 0; 64 * j < cnt; j += NW == 8 ? 4 : 1) {
         const int c = min(64 * j + lane, cnt - 1);
-        dma_b32(p.cand_ids + off + c, dst + 12 * kWMaxL + 256 * j);
+        dma_b32(p.cand_ids + off + c, dst + 12 * Cw::kMaxL + 256 * j);
       }
     }
   };
@@ -1262,14 +1273,16 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
     const int lane = threadIdx.x & 63;
     const int U = __builtin_amdgcn_readfirstlane(w_dup(i)[0]);
     const int* his = w_his(i);
+    constexpr int PPR = Cw::kMaxK / 4;                  // 16-byte pieces per logit row
+    constexpr int RPD = 64 / PPR;                         // rows per DMA
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = wave + 8 * j;                         // DMA n: rows 4n .. 4n + 3
-      if (4 * n >= U) break;
-      const int row = min(4 * n + (lane >> 4), U - 1);
-      const int pc = min(lane & 15, (KK >> 2) - 1);
+    for (int j = 0; j < Cw::kMaxL / RPD / NW; ++j) {
+      const int n = wave + NW * j;                        // DMA n: rows RPD n .. RPD n + RPD - 1
+      if (RPD * n >= U) break;
+      const int row = min(RPD * n + lane / PPR, U - 1);
+      const int pc = min(lane % PPR, (KK >> 2) - 1);
       const int id = min(max(his[row], 0), p.n_news - 1);
-      x2_dma_b128(p.logits + (size_t)id * KK + 4 * pc, sbase + kWOffLog + n * 1024);
+      x2_dma_b128(p.logits + (size_t)id * KK + 4 * pc, sbase + Cw::kOffLog + n * 1024);
     }
   };
   // the groups of impression i (wave 7; two 64-slot halves): its history ids are replaced by the
@@ -1278,16 +1291,16 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
   float du_E[2] = {1.f, 1.f}, du_P[2] = {1.f, 1.f};
   int du_slot[2] = {-1, -1}, du_i = -1;
   auto dedupe_merge = [&]() {
-    if (wave != 7 || du_i < 0) return;
+    if (wave != NW - 1 || du_i < 0) return;
     int* pcp = reinterpret_cast<int*>(w_prep(du_i));
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < Cw::kHalves; ++hh)
       if (du_slot[hh] >= 0)
         pcp[du_slot[hh]] |= (((__float_as_int(du_E[hh]) >> 23) & 255) << 8) | (((__float_as_int(du_P[hh]) >> 23) & 255) << 16);
     du_i = -1;
   };
   auto dedupe_prep = [&](int i) {
-    if (wave != 7 || i >= n_i) return;
+    if (wave != NW - 1 || i >= n_i) return;
     const int l = threadIdx.x & 63;
     int* his = w_his(i);
     int id[2];
@@ -1333,12 +1346,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
       if (uniq[hh]) {
         his[uidx] = id[hh];
         pc[uidx] = (ing ? mg : 1) | (keep[hh] ? 1 << 24 : 0);
-        pr[kWMaxL + uidx] = keep[hh] ? bv[hh] : 1e-30f;
+        pr[Cw::kMaxL + uidx] = keep[hh] ? bv[hh] : 1e-30f;
       }
       du_slot[hh] = uniq[hh] ? uidx : -1;
-      if (l + 64 * hh >= U) {              // past the groups: weight 0, units 2^-14
+      if (hh < Cw::kHalves && l + 64 * hh >= U) {   // past the groups: weight 0, units 2^-14
         pc[l + 64 * hh] = (113 << 8) | (113 << 16);
-        pr[kWMaxL + l + 64 * hh] = -INFINITY;
+        pr[Cw::kMaxL + l + 64 * hh] = -INFINITY;
       }
     }
     if (l == 0) w_dup(i)[0] = U;
@@ -1353,7 +1366,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
     const int c = sl ^ wswz(row);
     return (uint32_t)((c & 4) * 32 + 16 * (c & 3));
   };
-  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t& oC, unsigned& lv) {
+  constexpr int kCB = 8 / NW;                         // candidate DMA blocks (8 rows) per wave
+  auto item_offsets = [&](int i, int pass, uint32_t* oH, uint32_t* oC, unsigned& lv) {
     const int lane = threadIdx.x & 63;
     const bool live = i < n_i;
     int off = 0, cnt = 1;
@@ -1364,34 +1378,40 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
     lv = 0;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
-      const int row0 = 64 * jj + 8 * wave;
+      const int row0 = 8 * NW * jj + 8 * wave;
       if (live && row0 < U) lv |= 1u << jj;
       const int row = row0 + (lane >> 3);
       int h = live ? w_his(i)[min(row, U - 1)] : 0;
       h = min(max(h, 0), p.n_news - 1);
       oH[jj] = (uint32_t)h * rowBytes + chunk_off(row, lane & 7);
     }
-    {
-      const int row = 8 * wave + (lane >> 3);
-      if (live && WITH_CAND && 8 * wave < cnt - 64 * pass) lv |= 16u;
-      int c = (live && WITH_CAND) ? w_cand(i)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)] : 0;
+#pragma unroll
+    for (int cj = 0; cj < kCB; ++cj) {
+      const int row0 = 8 * NW * cj + 8 * wave;
+      const int row = row0 + (lane >> 3);
+      if (live && WITH_CAND && row0 < cnt - 64 * pass) lv |= 16u << cj;
+      int c = (live && WITH_CAND) ? w_cand(i)[min(64 * pass + min(row, cntp - 1), Cw::kMaxC - 1)] : 0;
       c = min(max(c, 0), p.n_news - 1);
-      oC = (uint32_t)c * rowBytes + chunk_off(row, lane & 7);
+      oC[cj] = (uint32_t)c * rowBytes + chunk_off(row, lane & 7);
     }
     lv = __builtin_amdgcn_readfirstlane(lv);
   };
-  auto dma_step = [&](const uint32_t* oH, uint32_t oC, unsigned lv, int sg, int slot) {
+  auto dma_step = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int sg, int slot) {
     if (lv == 0) return;
     const int so = (sg >> 1) * 256 + (sg & 1) * 64;
-    const unsigned m = sbase + slot * kWSlot;
+    const unsigned m = sbase + slot * Cw::kSlot;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       if (lv & (1u << jj)) {
-        x2_dma_row(oH[jj], tabB + so, m + jj * 8192 + wave * 1024);
-        if (WEIGHTED) x2_dma_row(oH[jj], prjB + so, m + kWPart + jj * 8192 + wave * 1024);
+        x2_dma_row(oH[jj], tabB + so, m + jj * 1024 * NW + wave * 1024);
+        if (WEIGHTED) x2_dma_row(oH[jj], prjB + so, m + Cw::kPart + jj * 1024 * NW + wave * 1024);
       }
     }
-    if (lv & 16u) x2_dma_row(oC, tabB + so, m + 2 * kWPart + (wave >> 1) * kWCTile + (wave & 1) * 1024);
+#pragma unroll
+    for (int cj = 0; cj < kCB; ++cj) {
+      const int row0 = 8 * NW * cj + 8 * wave;
+      if (lv & (16u << cj)) x2_dma_row(oC[cj], tabB + so, m + 2 * Cw::kPart + (row0 >> 4) * kWCTile + (row0 & 15) * kWRB);
+    }
   };
 
   // ---- per-lane LDS read offsets (fixed for the launch): as news_score_x2, 128-byte rows ----
@@ -1416,8 +1436,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
 
   // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kq + i][u] of the groups
   // u = 32 kb + 16 (e >> 2) + 4g + (e & 3)
-  u32x4 aH[4], aL[4];
-  int nkb = 4;
+  u32x4 aH[Cw::kNKb], aL[Cw::kNKb];
+  int nkb = Cw::kNKb;
   // softmax over the groups (model.py:176-181) of this wave's 16 interests, in registers (as
   // news_score_x2's softmax_inwave, up to 32 groups per lane)
   auto softmax_w = [&](int i, auto nss_c) {
@@ -1425,7 +1445,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
     const int k = 16 * kq + j;
-    const float* lgb = reinterpret_cast<const float*>(smem + kWOffLog);
+    const float* lgb = reinterpret_cast<const float*>(smem + Cw::kOffLog);
     const float* pr = w_prep(i);
     const int* pc = reinterpret_cast<const int*>(pr);
     const unsigned sh = P ? 16u : 8u;
@@ -1438,7 +1458,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
       wm[s] = (float)(code & 255u);
       un[s] = __uint_as_float(__builtin_amdgcn_ubfe(code, sh, 8) << 23);
       const float click = __uint_as_float((code >> 24) * 0x3f800000u);
-      v[s] = __builtin_fmaf(lgb[u * kWMaxK + min(k, KK - 1)], click, pr[kWMaxL + u]);
+      v[s] = __builtin_fmaf(lgb[u * Cw::kMaxK + min(k, KK - 1)], click, pr[Cw::kMaxL + u]);
       mx = fmaxf(mx, v[s]);
     }
     mx = x_rows4_max(mx);
@@ -1466,7 +1486,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
       aL[m >> 2][m & 3] = lv2;
     }
 #pragma unroll
-    for (int kb = NSS / 8; kb < 4; ++kb) {
+    for (int kb = NSS / 8; kb < Cw::kNKb; ++kb) {
       aH[kb] = u32x4{0u, 0u, 0u, 0u};
       aL[kb] = u32x4{0u, 0u, 0u, 0u};
     }
@@ -1476,50 +1496,53 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
   // finished pass, lane (kq4, c) interests [16 kq4, 16 kq4 + 16), the 4 lane rows by permlanes
   int pend_off = -1, pend_cnt = 0;
   auto s7 = [&]() {
-    if (wave < 4) return;
+    if (wave < NW / 2) return;
     const int lane = threadIdx.x & 63;
     const int cl = lane & 15, kq4 = lane >> 4;
-    const int c = 16 * (wave & 3) + cl;
-    const float* F = reinterpret_cast<const float*>(smem + kWOffF);
-    float lg[16], m[16];
+    const float* F = reinterpret_cast<const float*>(smem + Cw::kOffF);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int o = c * 64 + ((16 * kq4 + j) ^ cl);
-      m[j] = F[o] * uc_pend;
-      if constexpr (WEIGHTED) lg[j] = F[4096 + o] * uc_pend;
-    }
-    float sc;
-    if constexpr (WEIGHTED) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) mx = fmaxf(mx, lg[j]);
-      mx = x_rows4_max(mx);
-      float sm = 0.f, num = 0.f;
+    for (int rnd = 0; rnd < 8 / NW; ++rnd) {
+      const int c = 16 * ((wave - NW / 2) + (NW / 2) * rnd) + cl;
+      float lg[16], m[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        if (16 * kq4 + j < KK) {
-          const float pe = x2_exp(lg[j] - mx);
-          sm += pe;
-          num = __builtin_fmaf(pe, m[j], num);
-        }
+        const int o = c * Cw::kMaxK + (((16 * kq4 + j) ^ cl) & (Cw::kMaxK - 1));
+        m[j] = F[o] * uc_pend[rnd];
+        if constexpr (WEIGHTED) lg[j] = F[Cw::kFP + o] * uc_pend[rnd];
       }
-      sm = x_rows4_sum(sm);
-      num = x_rows4_sum(num);
-      sc = num * __builtin_amdgcn_rcpf(sm);
-    } else {
-      if (p.score_type == MINER_SCORE_MAX) {
+      float sc;
+      if constexpr (WEIGHTED) {
         float mx = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) mx = fmaxf(mx, m[j]);
-        sc = x_rows4_max(mx);
-      } else {
-        float sm = 0.f;
+        for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) mx = fmaxf(mx, lg[j]);
+        mx = x_rows4_max(mx);
+        float sm = 0.f, num = 0.f;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) sm += m[j];
-        sc = x_rows4_sum(sm) / (float)KK;
+        for (int j = 0; j < 16; ++j) {
+          if (16 * kq4 + j < KK) {
+            const float pe = x2_exp(lg[j] - mx);
+            sm += pe;
+            num = __builtin_fmaf(pe, m[j], num);
+          }
+        }
+        sm = x_rows4_sum(sm);
+        num = x_rows4_sum(num);
+        sc = num * __builtin_amdgcn_rcpf(sm);
+      } else {
+        if (p.score_type == MINER_SCORE_MAX) {
+          float mx = -INFINITY;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) mx = fmaxf(mx, m[j]);
+          sc = x_rows4_max(mx);
+        } else {
+          float sm = 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) if (16 * kq4 + j < KK) sm += m[j];
+          sc = x_rows4_sum(sm) / (float)KK;
+        }
       }
+      if (kq4 == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
     }
-    if (kq4 == 0 && c < pend_cnt) p.scores[pend_off + c] = sc;
   };
 
   f32x4 acc[4];
@@ -1529,11 +1552,11 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
     constexpr int NT = decltype(nt_c)::value;
     FRESH_LANE_IDS();
     const int g = lane >> 4, i = lane & 15;
-    const char* slot = smem + (t & 1) * kWSlot;
-    const char* part = slot + P * kWPart;
+    const char* slot = smem + (t & 1) * Cw::kSlot;
+    const char* part = slot + P * Cw::kPart;
     f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 0; kb < Cw::kNKb; ++kb) {
       if (kb >= nkb) break;
       u32x4 eH[2], eL[2];
 #pragma unroll
@@ -1555,7 +1578,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
             make_float4(hx[ctl][0] * mui_scale, hx[ctl][1] * mui_scale, hx[ctl][2] * mui_scale, hx[ctl][3] * mui_scale);
     }
     if constexpr (NT > 0) {
-      const char* cpart = slot + 2 * kWPart;
+      const char* cpart = slot + 2 * Cw::kPart;
       uint2 cH_[NT][2], cL_[NT][2];
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
@@ -1599,10 +1622,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
   };
 
   // ---- prologue ----
-  for (int o = (int)threadIdx.x * 16; o < kWRing; o += kThreads * 16)      // rows no DMA writes read as 0
+  for (int o = (int)threadIdx.x * 16; o < Cw::kRing; o += Cw::kThr * 16)      // rows no DMA writes read as 0
     *reinterpret_cast<u32x4*>(smem + o) = u32x4{0u, 0u, 0u, 0u};
-  for (int o = (int)threadIdx.x * 16; o < kWLogB; o += kThreads * 16)      // stale logit rows stay finite
-    *reinterpret_cast<u32x4*>(smem + kWOffLog + o) = u32x4{0u, 0u, 0u, 0u};
+  for (int o = (int)threadIdx.x * 16; o < Cw::kLogB; o += Cw::kThr * 16)      // stale logit rows stay finite
+    *reinterpret_cast<u32x4*>(smem + Cw::kOffLog + o) = u32x4{0u, 0u, 0u, 0u};
   for (int i = 0; i < 3; ++i) issue_L0(i);
   vm_wait_all();
   raw_barrier();
@@ -1615,7 +1638,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
   issue_L2(0);
   vm_wait_all();
   raw_barrier();
-  uint32_t cH[2], cC, nH[2] = {0u, 0u}, nC = 0u;
+  uint32_t cH[2], cC[kCB], nH[2] = {0u, 0u}, nC[kCB] = {};
   unsigned cLv = 0, nLv = 0;
   item_offsets(0, 0, cH, cC, cLv);
   dma_step(cH, cC, cLv, 0, 0);
@@ -1639,7 +1662,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
         vm_wait_all();
         raw_barrier();
         if (cp == 0 && sg == 1) dedupe_merge();      // before this step's DMAs: the unit loads have landed
-        if (sg == 0) asm volatile("" : "+v"(uc_pend));  // the candidate units' load waited for here, not behind the DMAs
+        if (sg == 0) {                // the candidate units' load waited for here, not behind the DMAs
+#pragma unroll
+          for (int rnd = 0; rnd < 8 / NW; ++rnd) asm volatile("" : "+v"(uc_pend[rnd]));
+        }
         if (sg + 1 < nst) {
           dma_step(cH, cC, cLv, sg + 1, (t + 1) & 1);
         } else {
@@ -1651,8 +1677,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
           pend_off = -1;
           if (cp == 0) {
             using std::integral_constant;
-            if (nkb <= 2) softmax_w(ci, integral_constant<int, 16>{});
-            else softmax_w(ci, integral_constant<int, 32>{});
+            if constexpr (NW == 8) {
+              if (nkb <= 2) softmax_w(ci, integral_constant<int, 16>{});
+              else softmax_w(ci, integral_constant<int, 32>{});
+            } else {
+              softmax_w(ci, integral_constant<int, 16>{});
+            }
             dedupe_prep(ci + 1);
             issue_L0(ci + 3);
             issue_L1(ci + 2);
@@ -1664,10 +1694,13 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
         }
         compute(ci, sg, need_c, mui_o, ntile);
       }
-      if (WITH_CAND && wave >= 4) {
-        const int c = 16 * (wave & 3) + (int)(threadIdx.x & 15);
-        const int id = w_cand(ci)[min(64 * cp + min(c, max(cntp, 1) - 1), kMaxCand - 1)];
-        uc_pend = p.unit_t[min(max(id, 0), p.n_news - 1)];
+      if (WITH_CAND && wave >= NW / 2) {
+#pragma unroll
+        for (int rnd = 0; rnd < 8 / NW; ++rnd) {
+          const int c = 16 * ((wave - NW / 2) + (NW / 2) * rnd) + (int)(threadIdx.x & 15);
+          const int id = w_cand(ci)[min(64 * cp + min(c, max(cntp, 1) - 1), Cw::kMaxC - 1)];
+          uc_pend[rnd] = p.unit_t[min(max(id, 0), p.n_news - 1)];
+        }
       }
       if constexpr (WITH_CAND) {
         // pass done: the partial M / Lg of every wave -> F[P][c][k ^ (c & 15)] (S7 after the next barrier)
@@ -1675,14 +1708,14 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
         const int j = lane & 15, g = lane >> 4;
         if (path_live && k_live) {
           const float pub_scale = kSA * __builtin_amdgcn_rcpf(kap);
-          float* F = reinterpret_cast<float*>(smem + kWOffF) + P * 4096;
+          float* F = reinterpret_cast<float*>(smem + Cw::kOffF) + P * Cw::kFP;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (q < ntile) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const int c = 16 * q + 4 * g + e;
-                F[c * 64 + ((16 * kq + j) ^ (c & 15))] = acc[q][e] * pub_scale;
+                F[c * Cw::kMaxK + (((16 * kq + j) ^ (c & 15)) & (Cw::kMaxK - 1))] = acc[q][e] * pub_scale;
               }
             }
           }
@@ -1692,7 +1725,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2w(X2Params p) {
       pend_cnt = cntp;
       cH[0] = nH[0];
       cH[1] = nH[1];
-      cC = nC;
+#pragma unroll
+      for (int cj = 0; cj < kCB; ++cj) cC[cj] = nC[cj];
       cLv = nLv;
     }
   }
@@ -1717,21 +1751,32 @@ int x2_num_cus() {
 
 inline bool al16(const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; }
 
-int x2w_launch(void* stream, const X2Params& prm) {
+template <int NW>
+int x2w_launch_nw(void* stream, const X2Params& prm) {
   void (*kern)(X2Params) = nullptr;
   const bool rg = prm.cand_off != nullptr;
   switch (prm.score_type) {
-    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2w<MINER_SCORE_WEIGHTED, true> : news_score_x2w<MINER_SCORE_WEIGHTED, false>; break;
-    case MINER_SCORE_NONE: kern = news_score_x2w<MINER_SCORE_NONE, false>; break;
-    default: kern = rg ? news_score_x2w<MINER_SCORE_MAX, true> : news_score_x2w<MINER_SCORE_MAX, false>; break;
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2w<MINER_SCORE_WEIGHTED, true, NW> : news_score_x2w<MINER_SCORE_WEIGHTED, false, NW>; break;
+    case MINER_SCORE_NONE: kern = news_score_x2w<MINER_SCORE_NONE, false, NW>; break;
+    default: kern = rg ? news_score_x2w<MINER_SCORE_MAX, true, NW> : news_score_x2w<MINER_SCORE_MAX, false, NW>; break;
   }
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XW<NW>::kLds);
   if (e != hipSuccess) return (int)e;
-  int grid = x2_num_cus();
+  int grid = x2_num_cus() * (8 / NW);
   if (grid > prm.B) grid = prm.B;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), kWLds, static_cast<hipStream_t>(stream), prm);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), XW<NW>::kLds, static_cast<hipStream_t>(stream), prm);
   e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;
+}
+int x2w_launch(void* stream, const X2Params& prm) { return x2w_launch_nw<8>(stream, prm); }
+
+// the two-workgroups-per-CU form (A/B: MINER_X2_W4=1): K <= 32, L <= 64, dense C <= 256, no eval loss
+#ifndef X2_W4
+#define X2_W4 0
+#endif
+bool x2w4_wanted(const X2Params& prm) {
+  const char* e = getenv("MINER_X2_W4");
+  return (e ? e[0] == '1' : X2_W4 != 0) && prm.K <= 32 && prm.L <= 64 && !prm.cand_off && prm.C <= 256 && !prm.dis_out;
 }
 
 #ifndef X2_FORCE_WIDE
@@ -1739,6 +1784,7 @@ int x2w_launch(void* stream, const X2Params& prm) {
 #endif
 int x2_launch(void* stream, const X2Params& prm) {
   if (prm.L > kMaxL || prm.K > kMaxK || (X2_FORCE_WIDE && !prm.dis_out)) return x2w_launch(stream, prm);
+  if (x2w4_wanted(prm)) return x2w_launch_nw<4>(stream, prm);
   void (*kern)(X2Params) = nullptr;
   int lds = kX2Lds;
   const bool rg = prm.cand_off != nullptr;
@@ -1833,7 +1879,7 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
   if (!table2 || !table_unit || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
   if (L <= 0 || d <= 0 || K <= 0) return MINER_EINVAL;
-  if (L > kWMaxL || K > kWMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
+  if (L > XW<8>::kMaxL || K > XW<8>::kMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
   if ((L > kMaxL || K > kMaxK) && disagree_out) return MINER_ESHAPE;   // the wide kernel writes mui instead
   if ((uint64_t)n_news * (uint64_t)d * 4u > 0xffffffffull) return MINER_ESHAPE;   // 32-bit row offsets
   if (score_type == MINER_SCORE_WEIGHTED && (!proj2 || !proj_unit)) return MINER_EINVAL;

@@ -354,6 +354,27 @@ def test_x2_ring3_equals_ring2(d, C, monkeypatch):
     _ok(s3, ref, torch.float32, "ring-3 scores")
 
 
+@pytest.mark.parametrize("d,C,bias,mui", [(768, 40, False, False), (256, 40, True, True), (64, 5, False, True),
+                                          (768, 150, True, False)])
+def test_x2_two_workgroups_per_cu(d, C, bias, mui, monkeypatch):
+    """The two-workgroups-per-CU form of the pair-plane kernel (news_score_x2w<4>, MINER_X2_W4=1:
+    4 waves and 80 KB per workgroup, dense candidates <= 256) against the oracle at the fp32 bar:
+    scores and mui, with and without category bias, three candidate passes."""
+    monkeypatch.setenv("MINER_NEWS_FP32", "x2")
+    monkeypatch.setenv("MINER_X2_W4", "1")
+    B = 700
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(70 + d + C, B, 50, d, 3000, torch.float32, C=C)
+    hb = (torch.rand(hid.shape, device=DEV) - 0.5) if bias else None
+    nt = news.precompute(table, W1, Q, W2)
+    out = news.score(nt, hid, mask, cid, his_bias=hb, return_user=mui)
+    torch.cuda.synchronize()
+    s, m = out if mui else (out, None)
+    ref_mui, ref = _oracle(table, hid, mask, cid, None, W1, Q, W2, bias=hb)
+    _ok(s, ref, torch.float32, "scores")
+    if mui:
+        _ok(m, ref_mui, torch.float32, "mui")
+
+
 def test_x2_nan_logit_propagates(monkeypatch):
     """A NaN in a clicked slot's logit (here through the category bias) makes the reference's softmax
     over the history NaN for that impression (torch softmax propagates it, model.py:176-181), so every

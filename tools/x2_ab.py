@@ -36,12 +36,12 @@ def build(name, rev="-", *flags):
     print("built", lib, flush=True)
 
 
-def run(names, B=1_000_000, reps=5):
+def run(names, B=1_000_000, reps=5, d=768, n_news=104000):
     import torch
     from miner_amd import news, ops, synthetic
     P, I = ctypes.c_void_p, ctypes.c_int
     dev = "cuda:0"
-    L, C, d, K, Dc, n_news = 50, 40, 768, 32, 200, 104000
+    L, C, K, Dc = 50, 40, 32, 200
     table = synthetic.news_table(3, n_news, d, device=dev)
     beh = synthetic.behaviors(3, 0, B, L=L, n_news=n_news, C=C, device=dev)
     W1, Q, W2 = synthetic.init_weights(3, d, Dc, K, device=dev)
@@ -91,9 +91,16 @@ if __name__ == "__main__":
     if a and a[0] == "--build":
         build(*a[1:])
     else:
-        B = 1_000_000
-        if "--B" in a:
-            i = a.index("--B")
-            B = int(a[i + 1])
-            a = a[:i] + a[i + 2:]
-        run(a, B)
+        B, d, nn = 1_000_000, 768, 104000
+        for flag in ("--B", "--d", "--n-news"):
+            if flag in a:
+                i = a.index(flag)
+                v = int(a[i + 1])
+                a = a[:i] + a[i + 2:]
+                if flag == "--B":
+                    B = v
+                elif flag == "--d":
+                    d = v
+                else:
+                    nn = v
+        run(a, B, d=d, n_news=nn)
