@@ -51,6 +51,18 @@ constexpr float kLnEps = 1e-12f;        // layer_norm_eps (model.py:255)
 #ifndef FF_PF32
 #define FF_PF32 1          // fp32 parity mode: 16 MFMAs per slab and matrix, one slab covers the latency
 #endif
+#ifndef FF_MQK_LDS
+#define FF_MQK_LDS 0   // experiment (bf16): mq / mk in two bf16 LDS images instead of fp32 registers, the
+                       // 29 vector slots read from L2 — the first step toward two impressions per CU
+#endif
+#ifndef FF_QFOLD
+// experiment (bf16): query_att folded into the query layer, qfs = x·W_fᵀ + b_f with W_f = Wqa·Wq and
+// b_f = Wqa·bq + bqa (model.py:416, :421: two linear maps in a row), packed in place of qa. Every
+// wave forms the logits of its own two heads from the x image (32 v_mfma_f32_16x16x32_bf16) instead
+// of a per-slab partial summed over the 8 waves through LDS: one barrier fewer per layer (8).
+#define FF_QFOLD 0
+#endif
+template <class T> constexpr bool kQFold = FF_QFOLD && sizeof(T) == 2 && !FF_MQK_LDS;
 
 // ---------------------------------------------------------------------------------------------
 // flat parameter blob (floats): FastformerEncoder.state_dict() order
@@ -127,7 +139,20 @@ __global__ void ff_pack_kernel(const float* __restrict__ src, T* __restrict__ ou
         const int ly = s >> 1;
         const int base = ly * blob::layer + ((s & 1) ? blob::ka_w : blob::qa_w);
         const int row = pi_row(rr);
-        if (row < kHeads) v = src[base + row * kH + 32 * j + cc];
+        if (kQFold<T> && !(s & 1)) {
+          // W_f = Wqa·Wq row-major [16][256] in the first 4096 elements of the qa slot
+          const int f = (int)(q % kSmallElems);
+          if (f < kHeads * kH) {
+            const int hd = f / kH, k = f % kH;
+            const float* wqa = src + base + hd * kH;
+            const float* wq = src + ly * blob::layer + blob::q_w + k;
+            double acc = 0.0;
+            for (int n = 0; n < kH; ++n) acc += (double)wqa[n] * (double)wq[(size_t)n * kH];
+            v = (float)acc;
+          }
+        } else if (row < kHeads) {
+          v = src[base + row * kH + 32 * j + cc];
+        }
       }
       outT[i] = (T)v;
     } else {
@@ -135,9 +160,19 @@ __global__ void ff_pack_kernel(const float* __restrict__ src, T* __restrict__ ou
       float v;
       if (q < (size_t)kVecSlots * kH) {
         int len;
-        const int off = vec_src((int)(q / kH), len);
+        const int slot = (int)(q / kH);
+        const int off = vec_src(slot, len);
         const int e = (int)(q % kH);
         v = e < len ? src[off + e] : 0.f;
+        if (kQFold<T> && slot >= vLayer && slot < vP1B && (slot - vLayer) % 12 == lvQaB && e < kHeads) {
+          // b_f = Wqa·bq + bqa
+          const int ly = (slot - vLayer) / 12;
+          const float* wqa = src + ly * blob::layer + blob::qa_w + e * kH;
+          const float* bq = src + ly * blob::layer + blob::q_b;
+          double acc = (double)v;
+          for (int n = 0; n < kH; ++n) acc += (double)wqa[n] * (double)bq[n];
+          v = (float)acc;
+        }
       } else {
         v = src[blob::pos + (q - (size_t)kVecSlots * kH)];
       }
@@ -172,12 +207,11 @@ constexpr int kSwBytes = kHeads * kMaxL * 4;           // [16 heads][64 rows] fp
 // parity mode has no room for them and reads them from L2
 template <class T> constexpr int kVecLds = sizeof(T) == 2 ? kVecSlots * kH * 4 : 0;
 template <class T> constexpr int kOffVec = 2 * kImg<T> + kRedBytes + kSwBytes + kH * 4;
-#ifndef FF_MQK_LDS
-#define FF_MQK_LDS 0   // experiment (bf16): mq / mk in two bf16 LDS images instead of fp32 registers, the
-                       // 29 vector slots read from L2 — the first step toward two impressions per CU
-#endif
 template <class T> constexpr bool kMqkLds = FF_MQK_LDS && sizeof(T) == 2;
-template <class T> constexpr int kLdsTotal = kOffVec<T> + (kMqkLds<T> ? 2 * kImg<T> : kVecLds<T>);
+// kQFold: both layers' folded query weights [layer][16 heads][256] bf16 after the vector slots
+constexpr int kFoldLds = kLayers * kHeads * kH * 2;
+template <class T> constexpr int kOffFold = kOffVec<T> + (kMqkLds<T> ? 2 * kImg<T> : kVecLds<T>);
+template <class T> constexpr int kLdsTotal = kOffFold<T> + (kQFold<T> ? kFoldLds : 0);
 static_assert(kWaves * kHeads * kMaxL * 4 <= kImg<__bf16>, "head partials fit a free image");
 
 // lane id from an opaque copy of threadIdx.x: per-lane addresses derived from it are recomputed in
@@ -449,6 +483,46 @@ __device__ __forceinline__ void head_softmax(const float* part, const float* bat
   }
 }
 
+// kQFold: the query softmax of heads 2·wave, 2·wave + 1 straight from the x image (model.py:421-426),
+// w = softmax((x·W_fᵀ + b_f) / 4 + ext). A = W_f rows: lane group g holds head 2·wave + (g & 1) in
+// all four of its rows; B = x rows 16·pt + n (the image chunk 4s + g is exactly the B fragment);
+// D register 0 of lane (n, g) = that head's logit at position 16·pt + n.
+__device__ __forceinline__ void qfold_softmax(const char* fold, char* img, const float* bf, float* swt, float extl,
+                                              int wave) {
+  static_assert(kMaxL == 64, "four 16-position tiles");
+  const int lane = fresh_lane();
+  const int n = lane & 15, g = lane >> 4;
+  const int hd = 2 * wave + (g & 1);
+  f32x4 acc[4];
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) acc[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < kNS; ++s) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(fold + hd * (kH * 2) + (4 * s + g) * 16);
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma16_bf16(a, *img_chunk<__bf16>(img, 16 * pt + n, 4 * s + g), acc[pt]);
+  }
+  const float b = bf[hd];
+  float sc[4], mx = -INFINITY;
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    sc[pt] = (acc[pt][0] + b) / 4.0f + __shfl(extl, 16 * pt + n);   // ext of position 16·pt + n
+    mx = fmaxf(mx, sc[pt]);
+  }
+  mx = row16_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    sc[pt] = __expf(sc[pt] - mx);
+    sum += sc[pt];
+  }
+  sum = row16_sum(sum);
+  if (g < 2) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) swt[hd * kMaxL + 16 * pt + n] = sc[pt] / sum;
+  }
+}
+
 // the wave's slab fragment of a head projection (qa / ka)
 template <class T>
 __device__ __forceinline__ void small_load(Frag<T>& a, const T* Watt, int wave) {
@@ -581,6 +655,8 @@ __device__ unsigned long long g_ff_imps;
 //   pooler     x in img0 (two swaps), img1 free: the next impression's E rows are DMA'd there
 // Barriers per layer: qfs partials, qks partials, wv, t, LN1 stats, a, h, LN2 stats, x' (9). The
 // head softmaxes need none: wave w owns heads 2w, 2w+1 and is the only reader of their weights.
+// kQFold: no qfs partials (8 barriers), x stays in cur: qks partials -> oth, wv -> cur, t -> oth,
+// a -> cur, h -> oth, x' -> cur, no swap (the pooler still finds x in img0).
 template <class T, bool GATHER>
 __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -601,6 +677,13 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
   if constexpr (kBf16 && !kMqkLds<T>) {
     float4* dst = reinterpret_cast<float4*>(smem + kOffVec<T>);
     for (int i = threadIdx.x; i < kVecSlots * kH / 4; i += kThreads) dst[i] = reinterpret_cast<const float4*>(gvecs)[i];
+  }
+  [[maybe_unused]] const char* foldL = smem + kOffFold<T>;
+  if constexpr (kQFold<T>) {     // W_f of both layers (the first 4096 elements of each qa slot) -> LDS
+    u32x4* dst = reinterpret_cast<u32x4*>(smem + kOffFold<T>);
+    constexpr int kPer = kHeads * kH * 2 / 16;
+    for (int i = threadIdx.x; i < kLayers * kPer; i += kThreads)
+      dst[i] = reinterpret_cast<const u32x4*>(small + (size_t)(2 * (i / kPer)) * kSmallElems)[i % kPer];
   }
   const T* __restrict__ hist = static_cast<const T*>(p.hist);
   const int L = p.L;
@@ -672,7 +755,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       }
       const T* const W[2] = {big + bmQ * kMat, big + bmK * kMat};
       ring_load<T, 2>(rq, W, wave);
-      small_load<T>(sq, small, wave);
+      if constexpr (!kQFold<T>) small_load<T>(sq, small, wave);
       small_load<T>(sk, small + kSmallElems, wave);
     }
     layer_norm<T>(x, red, vecs, vLn0W, vLn0B, wave);
@@ -694,6 +777,11 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       const T* Wl = big + (size_t)ly * 6 * kMat;
       const int vb = vLayer + 12 * ly;
       const int h = fresh_lane() >> 5;
+      // kQFold keeps x in `cur` for the whole layer: the buffers after the query softmax swap roles
+      char* bA = kQFold<T> ? oth : cur;
+      char* bB = kQFold<T> ? cur : oth;
+      if constexpr (kQFold<T>)
+        qfold_softmax(foldL + ly * (kHeads * kH * 2), cur, vecs + (vb + lvQaB) * kH, swt, ms.extl, wave);
 
       // G12: mixed query / key layers (model.py:416-417)
       f32x16 qk[2][2];
@@ -722,11 +810,13 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       FF_STAMP(1);
 
       // query attention -> pooled query (model.py:421-433); partials in oth
-      if constexpr (kMqkLds<T>) tile_load(imgq, mq);
-      head_partial<T>(reinterpret_cast<float*>(oth), sq, mq, wave);
-      __syncthreads();
-      FF_STAMP(2);
-      head_softmax<T>(reinterpret_cast<float*>(oth), vecs + (vb + lvQaB) * kH, swt, ms.extl, wave);
+      if constexpr (!kQFold<T>) {
+        if constexpr (kMqkLds<T>) tile_load(imgq, mq);
+        head_partial<T>(reinterpret_cast<float*>(oth), sq, mq, wave);
+        __syncthreads();
+        FF_STAMP(2);
+        head_softmax<T>(reinterpret_cast<float*>(oth), vecs + (vb + lvQaB) * kH, swt, ms.extl, wave);
+      }
       FF_STAMP(3);
       {
         float pq[16];
@@ -739,12 +829,12 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
           mk[1][e] *= pq[e];
         }
       }
-      // key attention -> pooled key (model.py:439-447); partials in cur (x image dead)
+      // key attention -> pooled key (model.py:439-447); partials in bA (cur: x is dead after G12)
       if constexpr (kMqkLds<T>) tile_store<T>(imgk, mk, wave);
-      head_partial<T>(reinterpret_cast<float*>(cur), sk, mk, wave);
+      head_partial<T>(reinterpret_cast<float*>(bA), sk, mk, wave);
       __syncthreads();
       FF_STAMP(4);
-      head_softmax<T>(reinterpret_cast<float*>(cur), vecs + (vb + lvKaB) * kH, swt, ms.extl, wave);
+      head_softmax<T>(reinterpret_cast<float*>(bA), vecs + (vb + lvKaB) * kH, swt, ms.extl, wave);
       FF_STAMP(5);
       {
         const T* const W[1] = {Wl + bmT * kMat};   // G3's first slabs, behind the pooled key and a barrier
@@ -763,7 +853,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
           wv[0][e] = pk[e] * mq[0][e];
           wv[1][e] = pk[e] * mq[1][e];
         }
-        tile_store<T>(oth, wv, wave);
+        tile_store<T>(bB, wv, wave);
       }
       __syncthreads();
       FF_STAMP(6);
@@ -772,7 +862,7 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       f32x16 t[1][2];
       {
         const T* const W[1] = {Wl + bmT * kMat};
-        gemm_run<T, 1>(t, oth, r1, W, wave);
+        gemm_run<T, 1>(t, bB, r1, W, wave);
         const T* const Wn[1] = {Wl + bmO * kMat};
         ring_load<T, 1>(r1, Wn, wave);
       }
@@ -780,14 +870,14 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       if constexpr (kMqkLds<T>) tile_load(imgq, mq);
       t[0][0] += mq[0];
       t[0][1] += mq[1];
-      tile_store<T>(cur, t[0], wave);
+      tile_store<T>(bA, t[0], wave);
       __syncthreads();
       FF_STAMP(7);
 
       // G4: BertSelfOutput — LayerNorm(dense(t) + x)
       {
         const T* const W[1] = {Wl + bmO * kMat};
-        gemm_run<T, 1>(t, cur, r1, W, wave);
+        gemm_run<T, 1>(t, bA, r1, W, wave);
         const T* const Wn[1] = {Wl + bmI * kMat};
         ring_load<T, 1>(r1, Wn, wave);
       }
@@ -795,33 +885,33 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       x[0] += t[0][0];
       x[1] += t[0][1];
       layer_norm<T>(x, red, vecs, vb + lvLn1W, vb + lvLn1B, wave);   // x := a
-      tile_store<T>(oth, x, wave);
+      tile_store<T>(bB, x, wave);
       __syncthreads();
       FF_STAMP(8);
 
       // G5: BertIntermediate — gelu(dense(a))
       {
         const T* const W[1] = {Wl + bmI * kMat};
-        gemm_run<T, 1>(t, oth, r1, W, wave);
+        gemm_run<T, 1>(t, bB, r1, W, wave);
         const T* const Wn[1] = {Wl + bmO2 * kMat};
         ring_load<T, 1>(r1, Wn, wave);
       }
       add_vec(t[0], vecs, vb + lvIB, wave, h);
       gelu_tile<T>(t[0][0]);
       gelu_tile<T>(t[0][1]);
-      tile_store<T>(cur, t[0], wave);
+      tile_store<T>(bA, t[0], wave);
       __syncthreads();
       FF_STAMP(9);
 
       // G6: BertOutput — LayerNorm(dense(h) + a)
       {
         const T* const W[1] = {Wl + bmO2 * kMat};
-        gemm_run<T, 1>(t, cur, r1, W, wave);
+        gemm_run<T, 1>(t, bA, r1, W, wave);
         // next: the following layer's q / k, or the pooler's att_fc1 (first ring slot)
         if (ly + 1 < kLayers) {
           const T* const Wn[2] = {Wl + (6 + bmQ) * kMat, Wl + (6 + bmK) * kMat};
           ring_load<T, 2>(rq, Wn, wave);
-          small_load<T>(sq, small + (size_t)(2 * ly + 2) * kSmallElems, wave);
+          if constexpr (!kQFold<T>) small_load<T>(sq, small + (size_t)(2 * ly + 2) * kSmallElems, wave);
           small_load<T>(sk, small + (size_t)(2 * ly + 3) * kSmallElems, wave);
         } else {
           const T* const Wn[1] = {big + (size_t)12 * kMat};
@@ -832,10 +922,10 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       x[0] += t[0][0];
       x[1] += t[0][1];
       layer_norm<T>(x, red, vecs, vb + lvLn2W, vb + lvLn2B, wave);
-      tile_store<T>(oth, x, wave);
+      tile_store<T>(bB, x, wave);
       __syncthreads();
       FF_STAMP(10);
-      char* tmp = cur; cur = oth; oth = tmp;
+      if constexpr (!kQFold<T>) { char* tmp = cur; cur = oth; oth = tmp; }
     }
 
     // ---- loads for later, short-latency ones first: vmcnt is in order, so anything issued after

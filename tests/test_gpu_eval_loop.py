@@ -25,10 +25,19 @@ def _setup(device):
     return table, W1, Q, W2
 
 
-@pytest.mark.parametrize("scorer", ["news", "gather"])
-def test_eval_loop_matches_oracle(scorer):
-    table, W1, Q, W2 = _setup(DEV)
-    beh = synthetic.behaviors(5, 0, CFG["n"], L=CFG["L"], n_news=CFG["n_news"], ragged=CFG["ragged"], device=DEV)
+WIDE = dict(CFG, n=300, L=100, K=64, ragged=(2, 100))
+
+
+@pytest.mark.parametrize("scorer,cfg", [("news", CFG), ("gather", CFG), ("news", WIDE)],
+                         ids=["news", "gather", "news-wide"])
+def test_eval_loop_matches_oracle(scorer, cfg):
+    """'news-wide' (K = 64 interests, 100-click histories) goes through news_score_x2w."""
+    from miner_amd import news
+    if cfg is WIDE:
+        assert news.wide_supported(torch.float32, cfg["L"], cfg["d"], cfg["Dc"], cfg["K"])
+    table = synthetic.news_table(5, cfg["n_news"], cfg["d"], device=DEV)
+    W1, Q, W2 = synthetic.init_weights(5, cfg["d"], cfg["Dc"], cfg["K"], device=DEV)
+    beh = synthetic.behaviors(5, 0, cfg["n"], L=cfg["L"], n_news=cfg["n_news"], ragged=cfg["ragged"], device=DEV)
     loss, scores = eval_loop.evaluate(ops.pack_weights(W1, Q, W2), table, beh, METRICS, chunk=256, scorer=scorer)
     # oracle: reference op order on the gathered rows, one impression at a time (ragged)
     t, w1, q, w2 = table.cpu(), W1.cpu(), Q.cpu(), W2.cpu()

@@ -66,9 +66,22 @@ def run(names, B=50000, reps=7):
             b.record()
             torch.cuda.synchronize()
             times[n].append(a.elapsed_time(b))
+    # the fp32 parity mode of the first build (exact fp32 arithmetic) as the accuracy yardstick
+    h0 = libs[names[0]]
+    t32 = table.float()
+    buf32 = torch.empty(h0.miner_fastformer_packed_bytes(0), dtype=torch.uint8, device=dev)
+    assert h0.miner_fastformer_pack(st, 0, params.data_ptr(), buf32.data_ptr()) == 0
+    ref = torch.empty_like(out[names[0]])
+    assert h0.miner_fastformer_score_gather(st, 0, t32.data_ptr(), n_news, beh.his_ids.data_ptr(), mask.data_ptr(),
+                                            beh.cand_ids.data_ptr(), beh.cand_offsets.data_ptr(), buf32.data_ptr(),
+                                            B, 50, 40, ref.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max())
     for n in names:
+        err = (out[n] - ref).abs()
         print(f"{n}: {statistics.median(times[n]):.3f} ms per {B} impressions, max |diff vs {names[0]}| "
-              f"{float((out[n] - out[names[0]]).abs().max()):.2e}", flush=True)
+              f"{float((out[n] - out[names[0]]).abs().max()):.2e}, vs fp32: max {float(err.max()):.2e} "
+              f"mean {float(err.mean()):.2e} (max |ref| {scale:.2e})", flush=True)
 
 
 if __name__ == "__main__":
