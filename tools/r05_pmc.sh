@@ -34,13 +34,13 @@ if [ "$WHICH" = dense ] || [ "$WHICH" = all ]; then
 fi
 if [ "$WHICH" = ff ] || [ "$WHICH" = all ]; then
   passes ffbf16 python3 "$R/tools/ff_time.py" --B 50000 --iters 2 || exit 1
-  python3 "$P" --batch 50000 --tag "ff_fusedIDF16bLb1E" --tag "ff_fused<__bf16, true>" --source fastformer \
+  python3 "$P" --batch 50000 --tag "ff_fusedIDF16bLb1E" --tag "ff_fused<__bf16, true>" --tag "ff_fused<bool _Accum" --source fastformer \
     --workload ff_L50_H256_C40_bf16 --kernel-name "ff_fused<bf16,gather>" \
     --out "$R/profiles/pmc_traffic_ff_bf16.json" "$O"/ffbf16_p* > "$O/traffic_ff_bf16.txt"
 fi
 if [ "$WHICH" = ffqfold ]; then     # the FF_QFOLD=1 build (tools/ff_flag_ab.py --build qfold -DFF_QFOLD=1)
   passes ffq python3 "$R/tools/ff_flag_ab.py" qfold || exit 1
-  python3 "$P" --batch 50000 --tag "ff_fusedIDF16bLb1E" --tag "ff_fused<__bf16, true>" --source fastformer \
+  python3 "$P" --batch 50000 --tag "ff_fusedIDF16bLb1E" --tag "ff_fused<__bf16, true>" --tag "ff_fused<bool _Accum" --source fastformer \
     --workload ff_L50_H256_C40_bf16_qfold --kernel-name "ff_fused<bf16,gather> FF_QFOLD=1" \
     --out "$R/profiles/pmc_traffic_ff_bf16_qfold.json" "$O"/ffq_p* > "$O/traffic_ff_bf16_qfold.txt"
 fi
