@@ -34,6 +34,12 @@ def hipcc() -> str:
 DEBUG_LIB = os.path.join(HERE, "libminer_hip_dbg.so")
 
 
+# per-file flags, each from an interleaved A/B on the box: hipcc's SLP vectorizer packs scalar fp32
+# work of these kernels into v_pk_* ops on operands in non-adjacent registers, and the v_mov pairs
+# it adds to gather them cost more VALU issue than the packing saves (profiles/r05_*_noslp_ab.txt)
+FILE_FLAGS = {"fastformer.hip": ["-fno-slp-vectorize"]}
+
+
 def _flags(debug: bool) -> list:
     return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed",
             *(["-DMINER_NEWS_DEBUG"] if debug else []), "-I", os.path.join(ROOT, "include")]
@@ -46,7 +52,7 @@ def _stamp(debug: bool) -> str:
         ver = subprocess.run([hipcc(), "--version"], capture_output=True, text=True, timeout=60).stdout.strip()
     except (OSError, subprocess.SubprocessError, RuntimeError):
         ver = "unknown"
-    return "\n".join([" ".join(_flags(debug)), ver])
+    return "\n".join([" ".join(_flags(debug)), repr(sorted(FILE_FLAGS.items())), ver])
 
 
 def _objdir(debug: bool) -> str:
@@ -83,7 +89,7 @@ def build_library(force: bool = False, verbose: bool = False, debug: bool = Fals
         if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_t):
             return obj
         tmp = obj + f".tmp{os.getpid()}"
-        cmd = [hipcc(), *flags, "-c", src, "-o", tmp]
+        cmd = [hipcc(), *flags, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", tmp]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         res = subprocess.run(cmd, capture_output=True, text=True)

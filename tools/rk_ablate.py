@@ -5,7 +5,8 @@ every build timed interleaved in one process on the same inputs (2048 users x 20
     python tools/rk_ablate.py --build 0 1 2 4 5 6 7 8     # CPU: tools/bisect/librk_abl<bits>.so
     python tools/rk_ablate.py 0 1 2 4 5 6 7 8 16s          # GPU; a trailing "s": the split form
                                                            # (miner_rank_topk_ws, MINER_RK_SPLIT=1);
-                                                           # "g": the 64-byte 4-stage geometry
+                                                           # "g": the 64-byte 4-stage geometry;
+                                                           # "<bits>n" builds without SLP vectorizing
 """
 import ctypes
 import os
@@ -25,8 +26,10 @@ def build(variants, extra=()):
     os.makedirs(OUT, exist_ok=True)
     for v in variants:
         lib = os.path.join(OUT, f"librk_abl{v}.so")
-        bits, _, w = str(v).partition("w")
-        wdef = [f"-DMINER_RK_DMAW={w}"] if w else []
+        v = str(v)
+        noslp = ["-fno-slp-vectorize"] if v.endswith("n") else []    # "<bits>n": without the SLP vectorizer
+        bits, _, w = v.rstrip("n").partition("w")
+        wdef = [f"-DMINER_RK_DMAW={w}", *noslp] if w else noslp
         subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-pass-failed",
                         f"-DMINER_RK_ABL={bits}", *wdef, *extra, "-I", os.path.join(ROOT, "include"),
                         os.path.join(ROOT, "miner_amd", "csrc", "corpus.hip"), "-o", lib], check=True)

@@ -1,6 +1,7 @@
 """The source identity a PMC counter file is bound to (tools/pmc_traffic.py writes it, bench.py checks
-it): sha256 over the repo-relative path and bytes of each kernel source a counter pass measured, so a
-kernel edited after its profiling pass cannot carry stale counters into a bench line."""
+it): sha256 over the repo-relative path and bytes of each kernel source a counter pass measured (and
+its per-file build flags), so a kernel edited after its profiling pass cannot carry stale counters
+into a bench line."""
 import hashlib
 import os
 
@@ -15,10 +16,23 @@ KERNEL_SOURCES = {
 }
 
 
+def _file_flags(rel: str) -> list:
+    """Extra hipcc flags miner_amd/build.py compiles this source with (they change the code as much
+    as an edit does)."""
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    from miner_amd.build import FILE_FLAGS
+    return FILE_FLAGS.get(os.path.basename(rel), [])
+
+
 def source_sha16(files) -> str:
     h = hashlib.sha256()
     for rel in files:
         h.update(rel.encode())
         with open(os.path.join(ROOT, rel), "rb") as f:
             h.update(f.read())
+        fl = _file_flags(rel)
+        if fl:
+            h.update(repr(fl).encode())
     return h.hexdigest()[:16]
