@@ -79,13 +79,30 @@ __device__ __forceinline__ void frag_store(T* p, const Frag<T>& f) {
 
 template <class T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
 
+// two fp32 -> one dword of 16-bit values (RNE), as a vector conversion: one v_cvt_pk_f16_f32 /
+// v_cvt_pk_bf16_f32 (gfx950); converting the halves one by one costs 3-4 VALU (two converts, a
+// shift and an OR) for the same bits
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+#ifndef MINER_PK_CVT
+#define MINER_PK_CVT 1   // A/B: 0 = the per-half conversions
+#endif
 __device__ __forceinline__ unsigned pack_f16x2(float lo, float hi) {
+#if MINER_PK_CVT
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){lo, hi}, f16x2v));
+#else
   _Float16 a = (_Float16)lo, b = (_Float16)hi;
   return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+#endif
 }
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+#if MINER_PK_CVT
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
+#else
   __bf16 a = (__bf16)lo, b = (__bf16)hi;
   return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+#endif
 }
 
 // accumulator tile (rows taken in pi order) -> 16 contiguous elements / slab fragment

@@ -200,7 +200,12 @@ struct FfParams {
 };
 
 // LDS carve (bytes): two activation images | LN / pooler exchange | head softmax weights | user
-template <class T> constexpr int kImg = kMaxL * kH * (int)sizeof(T);
+#ifndef FF_IMG_PAD
+#define FF_IMG_PAD 1   // activation images with 16-byte padded rows (addresses: a per-lane row base + immediates)
+#endif
+template <class T> constexpr int kRowB = kH * (int)sizeof(T);                  // bytes of one feature row
+template <class T> constexpr int kRowP = kRowB<T> + (FF_IMG_PAD ? 16 : 0);    // row stride of an activation image
+template <class T> constexpr int kImg = kMaxL * kRowP<T>;
 constexpr int kRedBytes = 2 * kWaves * kMaxL * 8;      // per-row reduction partials (kRedRow floats per row)
 constexpr int kSwBytes = kHeads * kMaxL * 4;           // [16 heads][64 rows] fp32
 // bf16: the 29 parameter-vector slots (biases, LayerNorm gains) live in LDS too (29 KiB); the fp32
@@ -222,11 +227,20 @@ __device__ __forceinline__ int fresh_lane() {
   return t & 63;
 }
 
-// image row `row`, 16-byte chunk c (XOR-swizzled within its 256-byte group: the 16 rows a
-// ds_read_b128 / ds_write_b128 lane group touches hit 16 different bank groups)
+// activation image row `row`, 16-byte chunk c: FF_IMG_PAD rows padded by 16 bytes (the 16 rows of a
+// ds_read_b128 / ds_write_b128 lane group start 4 banks apart, so they hit 16 different bank
+// groups, and the address is a per-lane row base plus a compile-time offset — no per-access VALU);
+// else 512-byte rows with the chunk XOR-swizzled within its 256-byte group
 template <class T>
 __device__ __forceinline__ u32x4* img_chunk(char* img, int row, int c) {
-  return reinterpret_cast<u32x4*>(img + row * (kH * (int)sizeof(T)) + ((c ^ (row & 15)) << 4));
+  if constexpr (FF_IMG_PAD) return reinterpret_cast<u32x4*>(img + row * kRowP<T> + (c << 4));
+  else return reinterpret_cast<u32x4*>(img + row * kRowB<T> + ((c ^ (row & 15)) << 4));
+}
+// the history rows as dma_history lands them: unpadded rows, chunk XOR-swizzled (an LDS-DMA
+// instruction writes its 1 KiB linearly; the swizzle is applied on the source address)
+template <class T>
+__device__ __forceinline__ const u32x4* hist_chunk(const char* img, int row, int c) {
+  return reinterpret_cast<const u32x4*>(img + row * kRowB<T> + ((c ^ (row & 15)) << 4));
 }
 // slab fragment (slab j, lane half h) of image row `row`, and its store
 template <class T>
@@ -303,9 +317,31 @@ __device__ __forceinline__ float xor32_max(float x) {
   return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
 }
 // sum over the 32 lanes of a lane half (every lane gets it); over all 64 lanes
-__device__ __forceinline__ float half_sum(float x) { return xor16_sum(row16_sum(x)); }
+// the DPP row reductions with bound_ctrl set: every pattern is a permutation within the row, so all
+// source lanes are valid and it changes nothing, but it lets hipcc fold each v_mov_b32_dpp into the
+// v_add / v_max that uses it (one VALU per step instead of two)
+#ifndef FF_DPP_FOLD
+#define FF_DPP_FOLD 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_b(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, FF_DPP_FOLD != 0));
+}
+__device__ __forceinline__ float row_sum16(float x) {
+  x += dpp_b<0xB1>(x);
+  x += dpp_b<0x4E>(x);
+  x += dpp_b<0x141>(x);
+  return x + dpp_b<0x140>(x);
+}
+__device__ __forceinline__ float row_max16(float x) {
+  x = fmaxf(x, dpp_b<0xB1>(x));
+  x = fmaxf(x, dpp_b<0x4E>(x));
+  x = fmaxf(x, dpp_b<0x141>(x));
+  return fmaxf(x, dpp_b<0x140>(x));
+}
+__device__ __forceinline__ float half_sum(float x) { return xor16_sum(row_sum16(x)); }
 __device__ __forceinline__ float wave_sum(float x) { return xor32_sum(half_sum(x)); }
-__device__ __forceinline__ float wave_max(float x) { return xor32_max(xor16_max(row16_max(x))); }
+__device__ __forceinline__ float wave_max(float x) { return xor32_max(xor16_max(row_max16(x))); }
 
 template <class T> __device__ __forceinline__ float ff_exp(float x) {
   if constexpr (sizeof(T) == 2) return __expf(x); else return expf(x);
@@ -389,11 +425,75 @@ static_assert(kMaxL * kRedRow * 4 <= kRedBytes, "reduction rows fit");
 // (mean, M2) of each lane's 16 features, combined exactly (Chan et al.) first with the other lane
 // half in registers (the row's 32 features of this wave), then over the 8 waves through LDS:
 // mean = Σ mean_g / G, M2 = Σ M2_g + n Σ (mean_g - mean)².
+#ifndef FF_LN_PK
+#define FF_LN_PK 1   // LayerNorm's per-element work on packed fp32 pairs (v_pk_add / v_pk_fma: half the VALU issue)
+#endif
+__device__ __forceinline__ f32x2 pair(const f32x16& v, int i) { return f32x2{v[2 * i], v[2 * i + 1]}; }
+
 template <class T>
 __device__ __forceinline__ void layer_norm(f32x16 (&v)[2], float* red, const float* vecs, int sw, int sb,
                                            int wave) {
   const int lane = fresh_lane();
   const int r = lane & 31, h = lane >> 5;
+#if FF_LN_PK
+  // the same statistics, combined in the same way; the sums over a lane's 16 features as pair trees
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    f32x2 a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = pair(v[mt], 2 * i) + pair(v[mt], 2 * i + 1);
+    const f32x2 sp = (a[0] + a[1]) + (a[2] + a[3]);
+    const float mean = (sp.x + sp.y) * (1.0f / 16.0f);
+    const f32x2 mm = {mean, mean};
+    f32x2 c0 = {0.f, 0.f}, c1 = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const f32x2 d0 = pair(v[mt], i) - mm, d1 = pair(v[mt], i + 1) - mm;
+      c0 = __builtin_elementwise_fma(d0, d0, c0);
+      c1 = __builtin_elementwise_fma(d1, d1, c1);
+    }
+    const f32x2 cs = c0 + c1;
+    const float m2 = cs.x + cs.y;
+    const float om = other_half(mean, h), om2 = other_half(m2, h);
+    const float dm = mean - om;
+    if (h == 0)
+      *reinterpret_cast<float2*>(red + (32 * mt + r) * kRedRow + 2 * wave) =
+          make_float2(0.5f * (mean + om), m2 + om2 + 8.0f * dm * dm);
+  }
+  const f32x16 g = load16(vecs + sw * kH + 32 * wave + 16 * h);
+  const f32x16 bb = load16(vecs + sb * kH + 32 * wave + 16 * h);
+  __syncthreads();
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const float4* row = reinterpret_cast<const float4*>(red + (32 * mt + r) * kRedRow);
+    float4 q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = row[i];
+    // (mean_w, M2_w) pairs of the 8 waves: one pair sum gives (Σ mean_w, Σ M2_w)
+    const f32x2 s01 = f32x2{q[0].x, q[0].y} + f32x2{q[0].z, q[0].w};
+    const f32x2 s23 = f32x2{q[1].x, q[1].y} + f32x2{q[1].z, q[1].w};
+    const f32x2 s45 = f32x2{q[2].x, q[2].y} + f32x2{q[2].z, q[2].w};
+    const f32x2 s67 = f32x2{q[3].x, q[3].y} + f32x2{q[3].z, q[3].w};
+    const f32x2 st = (s01 + s23) + (s45 + s67);
+    const float mean = st.x * (1.0f / kWaves);
+    const float mw[8] = {q[0].x, q[0].z, q[1].x, q[1].z, q[2].x, q[2].z, q[3].x, q[3].z};
+    float dev = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const float dlt = mw[w] - mean;
+      dev += dlt * dlt;
+    }
+    const float var = (st.y + 32.0f * dev) * (1.0f / (float)kH);
+    const float rstd = 1.0f / sqrtf(var + kLnEps);
+    const f32x2 rr = {rstd, rstd}, mm = {mean, mean};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x2 t = __builtin_elementwise_fma((pair(v[mt], i) - mm) * rr, pair(g, i), pair(bb, i));
+      v[mt][2 * i] = t.x;
+      v[mt][2 * i + 1] = t.y;
+    }
+  }
+#else
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     float s = 0.f;
@@ -439,6 +539,7 @@ __device__ __forceinline__ void layer_norm(f32x16 (&v)[2], float* red, const flo
 #pragma unroll
     for (int e = 0; e < 16; ++e) v[mt][e] = (v[mt][e] - mean) * rstd * g[e] + bb[e];
   }
+#endif
 }
 
 // per-wave partial of an additive-attention logit, (W_att · Xᵀ) over the wave's own slab:
@@ -509,14 +610,14 @@ __device__ __forceinline__ void qfold_softmax(const char* fold, char* img, const
     sc[pt] = (acc[pt][0] + b) / 4.0f + __shfl(extl, 16 * pt + n);   // ext of position 16·pt + n
     mx = fmaxf(mx, sc[pt]);
   }
-  mx = row16_max(mx);
+  mx = row_max16(mx);
   float sum = 0.f;
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt) {
     sc[pt] = __expf(sc[pt] - mx);
     sum += sc[pt];
   }
-  sum = row16_sum(sum);
+  sum = row_sum16(sum);
   if (g < 2) {
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) swt[hd * kMaxL + 16 * pt + n] = sc[pt] / sum;
@@ -748,7 +849,11 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
       for (int mt = 0; mt < 2; ++mt) {
         const int m = 32 * mt + r;
         Frag<T> f;
-        img_load<T>(f, img1, m, wave, h);
+        {
+          const int c0 = 32 * wave * (int)sizeof(T) / 16 + 16 * h * (int)sizeof(T) / 16;
+#pragma unroll
+          for (int i = 0; i < kNQ<T>; ++i) f.q[i] = *hist_chunk<T>(img1, m, c0 + i);
+        }
         const f32x16 e = frag_f32<T>(f);
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[mt][i] = m < L ? e[i] + posv[mt][i] : 0.0f;
