@@ -50,6 +50,13 @@ python3 "$P" --batch 50000 --tag "news_score_x2<0, false, 4, 2, false, false>" \
 python3 "$P" --batch 50000 --tag news_scoreIDF16bLi0ELb0ELi3ELi64ELi4ELi1E --tag "news_score<__bf16, 0, false, 3, 64, 4, 1>" \
   --workload news_L50_K32_d256_C40_N65238_bf16 --kernel-name "news_score<bf16,weighted,4 chunks,MIND>" \
   --out "$R/profiles/pmc_traffic_news_c2.json" "$O"/c2bf16_p* > "$O/traffic_c2bf16.txt"
+for i in 1 2 3; do   # news_score32 (MINER_NEWS_FP32=mfma32: the bench's fp32_mfma_exact sub-line)
+  pass="FETCH_SIZE"; [ $i = 2 ] && pass="WRITE_SIZE"; [ $i = 3 ] && pass="$SQ2"
+  echo "[profile] news32 pmc pass $i"
+  MINER_NEWS_FP32=mfma32 timeout -k 10 -s KILL 150 rocprofv3 --pmc $pass --kernel-trace -d "$O/n32_p$i" -o run --output-format csv -- \
+    python3 "$R/tools/news_once.py" fp32 "$B" 3 > "$O/n32_p$i.log" 2>&1
+done
+python3 "$P" --batch "$B" --news32 "$O"/n32_p* > "$O/traffic_news32.txt"
 cp "$R"/profiles/pmc_traffic*.json "$O/"
 echo "[profile] bench"
 timeout -k 10 400 python3 "$R/bench.py" > "$O/bench.json" 2> "$O/bench.err"
