@@ -27,7 +27,7 @@ def build(variants, extra=()):
     for v in variants:
         lib = os.path.join(OUT, f"librk_abl{v}.so")
         v = str(v)
-        noslp = ["-fno-slp-vectorize"] if v.endswith("n") else []    # "<bits>n": without the SLP vectorizer
+        noslp = ["-fno-slp-vectorize"] if "n" in v else []    # "<bits>n": without the SLP vectorizer
         bits, _, w = v.rstrip("n").partition("w")
         wdef = [f"-DMINER_RK_DMAW={w}", *noslp] if w else noslp
         subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-pass-failed",
@@ -64,8 +64,11 @@ def run(variants, U=2048, N=200000, reps=3):
         assert rc == 0, rc
 
     times = {v: [] for v in variants}
+    first = {}
     for v in variants:
         launch(v)
+        torch.cuda.synchronize()
+        first[v] = (ts.clone(), ti.clone())
     torch.cuda.synchronize()
     for _ in range(reps):
         for v in variants:
@@ -78,8 +81,9 @@ def run(variants, U=2048, N=200000, reps=3):
     fl = U * N * 4 * K * d
     for v in variants:
         t = statistics.median(times[v])
-        print(f"ABL={v:>3s}: {t:8.2f} ms  ({fl / t / 1e9 / 2500:.3f} of fp16 peak)  all {[round(x, 1) for x in times[v]]}",
-              flush=True)
+        same = bool(torch.equal(first[v][0], first[variants[0]][0]) and torch.equal(first[v][1], first[variants[0]][1]))
+        print(f"ABL={v:>3s}: {t:8.2f} ms  ({fl / t / 1e9 / 2500:.3f} of fp16 peak)  all {[round(x, 1) for x in times[v]]}"
+              f"  top-k identical to {variants[0]}: {same}", flush=True)
 
 
 if __name__ == "__main__":
