@@ -718,6 +718,40 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         Frag<T> af0, af1;
         frag_load(af0, Aw + r * AwS + 16 * h);
         if (nLs > 1) frag_load(af1, Aw + r * AwS + 32 + 16 * h); else frag_zero(af1);
+#ifndef MINER_S4_PF
+#define MINER_S4_PF 1   // fp32: the next d-tile's Eᵀ fragments (global loads) in flight during this tile's MFMAs
+#endif
+        if constexpr (!kBf16 && MINER_S4_PF) {
+          // Eᵀ fragment of d-tile `it`: lane (h, r) holds column 32·it + r of history rows 32·ls + 16h + e
+          // (rows >= L clamped: finite data times a zero weight). Every load unconditional (the tile index
+          // clamped), so hipcc's vmcnt waits stay counted instead of draining to 0.
+          auto load_e = [&](Frag<T>& bf, int it, int ls) {
+            const int i0 = min(it, ns - 1) * 32;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int l = min(32 * ls + 16 * h + e, L - 1);
+              bf.q[e >> 2][e & 3] = __float_as_uint(erow(l)[i0 + r]);
+            }
+          };
+          // two stages: rows 32..63 of tile it load during the MFMAs on rows 0..31, and rows 0..31 of
+          // tile it + 8 during those on rows 32..63 (one fragment in flight, no extra registers)
+          Frag<T> b0, b1;
+          load_e(b0, wave, 0);
+          for (int it = wave; it < ns; it += kWaves) {
+            const int i0 = it * 32;
+            load_e(b1, it, 1);
+            f32x16 acc = zero16();
+            mma_f<T, X6 && (MINER_X6_STAGES & 2)>(acc, af0, b0);
+            load_e(b0, it + kWaves, 0);
+            if (nLs > 1) mma_f<T, X6 && (MINER_X6_STAGES & 2)>(acc, af1, b1);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int k = acc_row(e, h);
+              muiL[k * msE + i0 + r] = from_f32<T>(acc[e]);
+              if (p.mui_out && k < K) p.mui_out[((size_t)b * K + k) * d + i0 + r] = acc[e];
+            }
+          }
+        } else
         for (int it = wave; it < ns; it += kWaves) {
           const int i0 = it * 32;
           f32x16 acc = zero16();
