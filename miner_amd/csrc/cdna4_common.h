@@ -297,6 +297,16 @@ __device__ __forceinline__ void split8_step(const Frag<float>& f, int st, u32x4&
 __device__ __forceinline__ f32x16 mfma32_bf16(const u32x4& a, const u32x4& b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
+// the six partial products of one 8-element step, smallest first (the order of mma_slab_x6)
+__device__ __forceinline__ void mma6_step(f32x16& acc, const u32x4& ah, const u32x4& am, const u32x4& al,
+                                          const u32x4& bh, const u32x4& bm, const u32x4& bl) {
+  acc = mfma32_bf16(al, bh, acc);
+  acc = mfma32_bf16(ah, bl, acc);
+  acc = mfma32_bf16(am, bm, acc);
+  acc = mfma32_bf16(am, bh, acc);
+  acc = mfma32_bf16(ah, bm, acc);
+  acc = mfma32_bf16(ah, bh, acc);
+}
 __device__ __forceinline__ void mma_slab_x6(f32x16& acc, const Frag<float>& a, const Frag<float>& b) {
 #pragma unroll
   for (int st = 0; st < 2; ++st) {

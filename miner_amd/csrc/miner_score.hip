@@ -94,6 +94,7 @@ struct Params {
   int eimg;     // bytes of the history image (bf16): the candidate rows may be staged there
   int dbg;      // ablation bits, honoured only by the -DMINER_STAMPS diagnostic build
   int part_ok;  // fp32: the mui region holds the S6 partial slabs (plain-store reduce); else LDS atomics
+  int offS1;    // fp32 full (bf16x6): the S1 history-operand planes (kS1Bytes)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -423,10 +424,21 @@ __device__ __forceinline__ float s7_score(const float (&lgv)[4], const float (&m
 // ---------------------------------------------------------------------------------------------
 // SHP 1: the MIND model shape compile-time (L = 50, Dc = 200, K = 32); X6 (fp32 only): S1 and
 // S5 on the bf16 matrix cores as bf16x6 (S4 stays on the fp32 MFMA) (the fp32-MFMA form stays selectable: MINER_DENSE_FP32=mfma32)
-template <class T, int MODE, int NS, bool GATHER, int SHP = 0, bool X6 = false>
+#ifndef MINER_S1_COOP
+#define MINER_S1_COOP 1   // fp32 bf16x6: the history operand of S1 split once per slab into LDS by all threads
+#endif
+constexpr int kS1Row = 80;                       // bytes per row of a split plane (32 bf16 + 16 pad: conflict-free b128)
+constexpr int kS1Plane = 64 * kS1Row;            // one plane of one slab (64 history rows)
+constexpr int kS1Slab = 3 * kS1Plane;            // hi | mid | lo
+constexpr int kS1Bytes = 4 * kS1Slab;            // two buffers of two slabs
+
+template <class T, int MODE, int NS, bool GATHER, int SHP = 0, bool X6 = false, bool S1C = false>
 __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kBf16 = sizeof(T) == 2;
+  // S1C: the fp32 bf16x6 form with S1's history operand cut once per slab into LDS (the host picks
+  // it where the carve holds one workgroup per CU anyway)
+  constexpr bool kS1Coop = S1C && !kBf16 && X6 && (MINER_X6_STAGES & 1) && MODE == kFull;
   // news-table gather mode (compile-time, so the dense instantiations carry no gather code)
   const int32_t* const his_ids = GATHER ? p.his_ids : nullptr;
   const int32_t* const cand_ids = GATHER ? p.cand_ids : nullptr;
@@ -511,8 +523,73 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
       // ---- S1: Pᵀ = tanh(W1[ct] · Eᵀ) -> P[l][c] in LDS -------------------------------------
       {
         FRESH_LANE_IDS();
+        // fp32 bf16x6 (kS1Coop): the history operand is the same for every wave, so its three bf16
+        // terms are cut once per slab by all 512 threads into LDS (two slabs per round, planes of
+        // 80-byte rows) instead of by each of the 7 MFMA waves in registers; products and their
+        // order per accumulator unchanged (bit-identical)
+        f32x16 cacc0 = zero16(), cacc1 = zero16();
+        constexpr bool coop = kS1Coop;
+        if constexpr (coop) {
+          // rounds of two slabs through two LDS buffers: round g + 1 is cut (its global loads in
+          // flight) while round g's products run, one barrier per round
+          const T* w1t = W1p + (size_t)min(wave, nct - 1) * ns * 1024;
+          Frag<T> ring1;
+          frag_load_tile(ring1, w1t, lane);
+          auto cut = [&](int g) {          // slabs g, g + 1 -> buffer (g / 2) & 1
+            char* sb = smem + p.offS1 + ((g >> 1) & 1) * (2 * kS1Slab);
+            const int row = tid >> 3, cb = tid & 7, sl = cb >> 2, c8 = (cb & 3) * 8;
+            if (g + sl < ns) {
+              const float4* src = reinterpret_cast<const float4*>(erow(min(row, L - 1)) + (g + sl) * 32 + c8);
+              const float4 x0 = src[0], x1 = src[1];
+              const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+              u32x4 hi, md, lo;
+#pragma unroll
+              for (int m = 0; m < 4; ++m) {
+                unsigned a, b, c;
+                split3_pair<true>(xv[2 * m], xv[2 * m + 1], a, b, c);
+                hi[m] = a;
+                md[m] = b;
+                lo[m] = c;
+              }
+              char* dst = sb + sl * kS1Slab + row * kS1Row + c8 * 2;
+              *reinterpret_cast<u32x4*>(dst) = hi;
+              *reinterpret_cast<u32x4*>(dst + kS1Plane) = md;
+              *reinterpret_cast<u32x4*>(dst + 2 * kS1Plane) = lo;
+            }
+          };
+          cut(0);
+          __syncthreads();
+          for (int g = 0; g < ns; g += 2) {
+            if (g + 2 < ns) cut(g + 2);
+            if (wave < nct) {
+              const char* sb = smem + p.offS1 + ((g >> 1) & 1) * (2 * kS1Slab);
+#pragma unroll
+              for (int s2 = 0; s2 < 2; ++s2) {
+                if (g + s2 < ns) {
+                  const Frag<T> a = ring1;
+                  frag_load_tile(ring1, w1t + min(g + s2 + 1, ns - 1) * 1024, lane);
+                  const char* base = sb + s2 * kS1Slab;
+#pragma unroll
+                  for (int st = 0; st < 2; ++st) {
+                    u32x4 ah, am, al;
+                    split8_step<false>(a, st, ah, am, al);
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt) {
+                      const char* q = base + (32 * rt + r) * kS1Row + (16 * h + 8 * st) * 2;
+                      const u32x4 bh = *reinterpret_cast<const u32x4*>(q);
+                      const u32x4 bm = *reinterpret_cast<const u32x4*>(q + kS1Plane);
+                      const u32x4 bl = *reinterpret_cast<const u32x4*>(q + 2 * kS1Plane);
+                      mma6_step(rt ? cacc1 : cacc0, ah, am, al, bh, bm, bl);
+                    }
+                  }
+                }
+              }
+            }
+            __syncthreads();                 // round g + 2 cut; round g's buffer read by every wave
+          }
+        }
         if (wave < nct) {
-          f32x16 acc0 = zero16(), acc1 = zero16();
+          f32x16 acc0 = cacc0, acc1 = cacc1;
           const T* w1t = W1p + (size_t)wave * ns * 1024;   // block (tile, slab 0)
           // rows >= L: finite, dropped in S3.  bf16: lane r takes history row pi(r), so the tanh'd
           // accumulator is directly the A operand of the fused S2 product (rows l in pi order)
@@ -522,7 +599,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           if constexpr (kBf16) frag_load(qa, Qp + r * (nct * 32) + wave * 32 + 16 * h);
           Frag<T> ring[PF1];
 #pragma unroll
-          for (int s = 0; s < PF1; ++s) frag_load_tile(ring[s], w1t + min(s, ns - 1) * 1024, lane);
+          for (int s = 0; s < PF1; ++s)
+            if (!coop) frag_load_tile(ring[s], w1t + min(s, ns - 1) * 1024, lane);
           if constexpr (kBf16) {
             // the history fragments of slab s+1 are read from LDS before slab s's MFMAs: read right
             // before use, every MFMA waited one LDS latency (lgkmcnt) — S1 was LDS-latency bound
@@ -559,7 +637,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
                 c1 = n1;
               }
             }
-          } else {
+          } else if (!coop) {
             int j = 0;
 #pragma unroll
             for (; j + PF1 <= ns; j += PF1) {
@@ -998,6 +1076,7 @@ inline int round16(int x) { return (x + 15) & ~15; }
 struct Carve {
   int MS, PS, offE, offZ, offP, offS, offMui, offAw, offPart, offLg, offMt, offAux, eimg, total;
   int part_ok;
+  int offS1;
 };
 
 // LDS carve (bytes).
@@ -1048,7 +1127,14 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   if (!bf) c.offPart = c.offMui;                   // fp32: the last chunk's partials (after its products)
   c.offAw = round16(c.offMui + r2);
   c.total = c.offAw + aw;
-  if (!bf && mode == kFull) {   // fp32 gather mode: the impression's history ids
+  if (!bf && mode == kFull && MINER_S1_COOP && (MINER_X6_STAGES & 1) && c.total > kLdsMax / 2) {
+    // the S1 history-operand planes: in the mui region behind P and S (free until S4; P is written
+    // after the S1 loop, S in S2), running on into Aw (written in S3) and past it where needed; only
+    // where the carve already holds one workgroup per CU (the planes would cost a second one)
+    c.offS1 = round16(c.offS + kMaxK * kMaxL * 4);
+    if (c.offS1 + kS1Bytes > c.total) c.total = c.offS1 + kS1Bytes;
+  }
+  if (!bf && mode == kFull) {   // fp32 gather mode: the impression's history ids (read during S1: after its planes)
     c.offAux = round16(c.total);
     c.total = c.offAux + kMaxL * 4;
   }
@@ -1079,9 +1165,9 @@ int num_cus() {
 
 inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <class T, int MODE, int NS, bool GATHER = false, int SHP = 0, bool X6 = false>
+template <class T, int MODE, int NS, bool GATHER = false, int SHP = 0, bool X6 = false, bool S1C = false>
 int launch(void* stream, const Params& prm, int lds) {
-  auto kern = miner_fused<T, MODE, NS, GATHER, SHP, X6>;
+  auto kern = miner_fused<T, MODE, NS, GATHER, SHP, X6, S1C>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   const int per_cu = kLdsMax / lds > 0 ? (kLdsMax / lds > 2 ? 2 : kLdsMax / lds) : 1;
@@ -1099,7 +1185,7 @@ int run(void* stream, int dtype, int mode, Params prm) {
   const Carve c = carve(dtype, mode, prm.L, prm.d, prm.Dc);
   prm.MS = c.MS; prm.PS = c.PS; prm.offE = c.offE; prm.offZ = c.offZ; prm.offP = c.offP; prm.offS = c.offS;
   prm.offMui = c.offMui; prm.offAw = c.offAw; prm.offPart = c.offPart; prm.offLg = c.offLg; prm.offMt = c.offMt;
-  prm.offAux = c.offAux; prm.eimg = c.eimg; prm.part_ok = c.part_ok;
+  prm.offAux = c.offAux; prm.eimg = c.eimg; prm.part_ok = c.part_ok; prm.offS1 = c.offS1;
   const bool gather = prm.his_ids != nullptr;
   if (dtype == MINER_DTYPE_BF16) {
     // config 3's model (d = 768, history 50, Dc = 200, K = 32), dense rows: the shape compile-time
@@ -1128,6 +1214,9 @@ int run(void* stream, int dtype, int mode, Params prm) {
     return gather ? launch<float, kFull, 0, true>(stream, prm, c.total) : launch<float, kFull, 0>(stream, prm, c.total);
   }
   if (mode == kTaa) return launch<float, kTaa, 0, false, 0, true>(stream, prm, c.total);
+  if (c.offS1 > 0)
+    return gather ? launch<float, kFull, 0, true, 0, true, true>(stream, prm, c.total)
+                  : launch<float, kFull, 0, false, 0, true, true>(stream, prm, c.total);
   return gather ? launch<float, kFull, 0, true, 0, true>(stream, prm, c.total) : launch<float, kFull, 0, false, 0, true>(stream, prm, c.total);
 }
 
