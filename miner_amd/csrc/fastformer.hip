@@ -346,6 +346,15 @@ __device__ __forceinline__ float wave_max(float x) { return xor32_max(xor16_max(
 template <class T> __device__ __forceinline__ float ff_exp(float x) {
   if constexpr (sizeof(T) == 2) return __expf(x); else return expf(x);
 }
+#ifndef FF_FAST_DIV
+#define FF_FAST_DIV 1   // bf16: 1/x and 1/sqrt(x) by v_rcp_f32 / v_rsq_f32 (~1 ulp) instead of IEEE division (~10 VALU)
+#endif
+template <class T> __device__ __forceinline__ float ff_rcp(float x) {
+  if constexpr (sizeof(T) == 2 && FF_FAST_DIV) return __builtin_amdgcn_rcpf(x); else return 1.0f / x;
+}
+template <class T> __device__ __forceinline__ float ff_rsqrt(float x) {
+  if constexpr (sizeof(T) == 2 && FF_FAST_DIV) return __builtin_amdgcn_rsqf(x); else return 1.0f / sqrtf(x);
+}
 template <class T> __device__ __forceinline__ float ff_tanh(float x) {
   if constexpr (sizeof(T) == 2) return tanh_fast(x); else return tanhf(x);
 }
@@ -484,7 +493,7 @@ __device__ __forceinline__ void layer_norm(f32x16 (&v)[2], float* red, const flo
       dev += dlt * dlt;
     }
     const float var = (st.y + 32.0f * dev) * (1.0f / (float)kH);
-    const float rstd = 1.0f / sqrtf(var + kLnEps);
+    const float rstd = ff_rsqrt<T>(var + kLnEps);
     const f32x2 rr = {rstd, rstd}, mm = {mean, mean};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -535,7 +544,7 @@ __device__ __forceinline__ void layer_norm(f32x16 (&v)[2], float* red, const flo
       dev += dlt * dlt;
     }
     const float var = (m2 + 32.0f * dev) * (1.0f / (float)kH);
-    const float rstd = 1.0f / sqrtf(var + kLnEps);
+    const float rstd = ff_rsqrt<T>(var + kLnEps);
 #pragma unroll
     for (int e = 0; e < 16; ++e) v[mt][e] = (v[mt][e] - mean) * rstd * g[e] + bb[e];
   }
@@ -580,7 +589,7 @@ __device__ __forceinline__ void head_softmax(const float* part, const float* bat
     const float mx = wave_max(s);
     const float ex = ff_exp<T>(s - mx);
     const float sum = wave_sum(ex);
-    swt[hd * kMaxL + lane] = ex / sum;
+    swt[hd * kMaxL + lane] = sizeof(T) == 2 && FF_FAST_DIV ? ex * ff_rcp<T>(sum) : ex / sum;
   }
 }
 
@@ -1083,8 +1092,14 @@ __global__ __launch_bounds__(kThreads) void ff_fused(FfParams p) {
         al[mt] = (mt ? ms.m1 : ms.m0) ? a : 0.0f;
       }
       const float tot = half_sum(al[0] + al[1]) + 1e-8f;
-      al[0] /= tot;
-      al[1] /= tot;
+      if constexpr (sizeof(T) == 2 && FF_FAST_DIV) {
+        const float it = ff_rcp<T>(tot);
+        al[0] *= it;
+        al[1] *= it;
+      } else {
+        al[0] /= tot;
+        al[1] /= tot;
+      }
       f32x16 u;
 #pragma unroll
       for (int e = 0; e < 16; ++e) u[e] = half_sum(al[0] * x[0][e] + al[1] * x[1][e]);

@@ -19,13 +19,14 @@ cd /tmp && export TMPDIR=/tmp
 SQ1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
 SQ2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE GRBM_COUNT"
 i=0
-for pass in "FETCH_SIZE" "WRITE_SIZE" "$SQ2" "$SQ1"; do
+[ -n "${SKIP_N32:-}" ] && PASSES="" || PASSES=1
+for pass in ${PASSES:+"FETCH_SIZE" "WRITE_SIZE" "$SQ2" "$SQ1"}; do
   i=$((i+1))
   echo "[final] news32 pmc pass $i"
   MINER_NEWS_FP32=mfma32 timeout -k 10 -s KILL 150 rocprofv3 --pmc $pass --kernel-trace -d "$O/n32_p$i" -o run --output-format csv -- \
     python3 "$R/tools/news_once.py" fp32 3000000 3 > "$O/n32_p$i.log" 2>&1 || { tail -5 "$O/n32_p$i.log"; exit 1; }
 done
-python3 "$R/tools/pmc_traffic.py" --batch 3000000 --news32 "$O"/n32_p* > "$O/traffic_news32.txt" || exit 1
+[ -n "$PASSES" ] && { python3 "$R/tools/pmc_traffic.py" --batch 3000000 --news32 "$O"/n32_p* > "$O/traffic_news32.txt" || exit 1; }
 echo "[final] bench"
 timeout -k 10 400 python3 "$R/bench.py" > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
 cp "$R"/profiles/pmc_traffic*.json "$O/"
