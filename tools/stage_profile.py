@@ -39,10 +39,12 @@ def main():
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--C", type=int, default=40)
     ap.add_argument("--kernel", default="miner", choices=["miner", "fastformer"])
+    ap.add_argument("--cflag", action="append", default=[], help="build: extra compiler flag (repeatable), "
+                    "e.g. -fno-slp-vectorize as miner_amd/build.py FILE_FLAGS gives fastformer.hip")
     args = ap.parse_args()
     lib = STAMP_LIB if not args.variant else STAMP_LIB.replace(".so", "_" + args.variant.replace(",", "_").replace("=", "") + ".so")
     if args.build:
-        build(["-D" + x for x in args.variant.split(",")] if args.variant else (), lib)
+        build([*(["-D" + x for x in args.variant.split(",")] if args.variant else ()), *args.cflag], lib)
         return
     os.environ["MINER_HIP_LIB"] = lib
     if args.kernel == "fastformer":
