@@ -5,6 +5,7 @@ launch of miner_score_news and the max score difference against the first build.
     python tools/news_flag_ab.py --build NAME [FLAGS...]                 # CPU: tools/bisect/libnews_NAME.so
     python tools/news_flag_ab.py [--cfg 3|2] [--B N] NAME1 NAME2 ...     # GPU (config 3: d 768, 104k news;
                                                                          #      config 2: d 256, 65,238 news)
+    python tools/news_flag_ab.py --pre NAME1 NAME2 ...                   # GPU: the fp32 precompute, config 3
 """
 import argparse
 import ctypes
@@ -26,6 +27,51 @@ def build(name, *flags):
                     *flags, "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "miner_amd", "csrc", "news.hip"),
                     "-o", lib], check=True)
     print("built", lib, flush=True)
+
+
+def run_pre(names, reps=9):
+    """fp32 per-news precompute (miner_news_precompute) of the config-3 table, 104,000 x 768: median ms
+    per call and max |logits / proj difference| against the first build."""
+    import torch
+    from miner_amd import ops, synthetic
+    P, I = ctypes.c_void_p, ctypes.c_int
+    dev = "cuda:0"
+    d, n_news, Dc, K = 768, 104000, 200, 32
+    g = torch.Generator(device=dev).manual_seed(36)
+    table = torch.randn((n_news, d), generator=g, device=dev) / d ** 0.5
+    W1, Q, W2 = synthetic.init_weights(36, d, Dc, K, device=dev)
+    pw = ops.pack_weights(W1, Q, W2, dtype=torch.float32)
+    st = torch.cuda.current_stream().cuda_stream
+    libs, lg, pj = {}, {}, {}
+    for n in names:
+        h = ctypes.CDLL(os.path.join(OUT, f"libnews_{n}.so"))
+        h.miner_news_precompute.argtypes = [P, I, P, I, P, I, I, I, P, P]
+        libs[n] = h
+        lg[n] = torch.empty((n_news, K), device=dev)
+        pj[n] = torch.empty((n_news, d), device=dev)
+
+    def launch(n):
+        rc = libs[n].miner_news_precompute(st, 0, table.data_ptr(), n_news, pw.buf.data_ptr(), d, Dc, K,
+                                           lg[n].data_ptr(), pj[n].data_ptr())
+        assert rc == 0, rc
+
+    times = {n: [] for n in names}
+    for n in names:
+        launch(n)
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        for n in names:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            launch(n)
+            b.record()
+            torch.cuda.synchronize()
+            times[n].append(a.elapsed_time(b))
+    for n in names:
+        dl = float((lg[n] - lg[names[0]]).abs().max() / lg[names[0]].abs().max())
+        dp = float((pj[n] - pj[names[0]]).abs().max() / pj[names[0]].abs().max())
+        print(f"{n}: precompute {statistics.median(times[n]):.3f} ms, max |diff vs {names[0]}| / max: logits {dl:.2e}, "
+              f"proj {dp:.2e}", flush=True)
 
 
 def run(names, cfg=3, B=None, reps=9):
@@ -85,6 +131,10 @@ if __name__ == "__main__":
         ap = argparse.ArgumentParser()
         ap.add_argument("--cfg", type=int, default=3)
         ap.add_argument("--B", type=int, default=None)
+        ap.add_argument("--pre", action="store_true", help="time the fp32 precompute instead of the scoring kernel")
         ap.add_argument("names", nargs="+")
         a = ap.parse_args()
-        run(a.names, a.cfg, a.B)
+        if a.pre:
+            run_pre(a.names)
+        else:
+            run(a.names, a.cfg, a.B)
