@@ -36,8 +36,11 @@ DEBUG_LIB = os.path.join(HERE, "libminer_hip_dbg.so")
 
 # per-file flags, each from an interleaved A/B on the box: hipcc's SLP vectorizer packs scalar fp32
 # work of these kernels into v_pk_* ops on operands in non-adjacent registers, and the v_mov pairs
-# it adds to gather them cost more VALU issue than the packing saves (profiles/r05_*_noslp_ab.txt)
-FILE_FLAGS = {"fastformer.hip": ["-fno-slp-vectorize"]}
+# it adds to gather them cost more VALU issue than the packing saves (profiles/r05_*_noslp_ab.txt);
+# news_x2.hip under the max-ILP machine scheduler: -0.54 % on the headline kernel, bit-identical
+# (profiles/r05_sched_strategy_ab.txt; the same strategy costs FastFormer +2.8 %)
+FILE_FLAGS = {"fastformer.hip": ["-fno-slp-vectorize"],
+              "news_x2.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
 def _flags(debug: bool) -> list:
