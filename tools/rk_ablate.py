@@ -28,7 +28,10 @@ def build(variants, extra=()):
         lib = os.path.join(OUT, f"librk_abl{v}.so")
         v = str(v)
         noslp = ["-fno-slp-vectorize"] if "n" in v else []    # "<bits>n": without the SLP vectorizer
-        bits, _, w = v.rstrip("n").partition("w")
+        # "<bits>i" / "<bits>m": the max-ILP / max-memory-clause machine scheduler
+        sched = [f for c, f in (("i", "max-ilp"), ("m", "max-memory-clause")) if c in v]
+        noslp += ["-mllvm", f"-amdgpu-sched-strategy={sched[0]}"] if sched else []
+        bits, _, w = v.rstrip("nim").partition("w")
         wdef = [f"-DMINER_RK_DMAW={w}", *noslp] if w else noslp
         subprocess.run([hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-pass-failed",
                         f"-DMINER_RK_ABL={bits}", *wdef, *extra, "-I", os.path.join(ROOT, "include"),
