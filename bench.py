@@ -868,6 +868,7 @@ def run_fastformer(args, rank, world, dev):
 # config 5: full-corpus ranking
 # ---------------------------------------------------------------------------------------------
 C5_L, C5_K, C5_N, C5_U, C5_TOPK = 200, 64, 200_000, 2048, 100
+C5_SHARE_U = 1_000_000 // 8          # config 5's users per GPU on 8 GPUs
 
 
 def corpus_cpu_baseline(seconds: float = 10.0):
@@ -1000,7 +1001,7 @@ def wide_news_subline(dev, steps=5, warmup=2):
                                    "max_abs_diff_x_rms": d_old}}
 
 
-def config5_subline(dev, steps=2, warmup=1):
+def config5_subline(dev, steps=2, warmup=1, share_users=C5_SHARE_U):
     """BASELINE config 5 (full-corpus ranking: 2048 users x 200k news, L=200, K=64, fp16, top-100) measured
     inside the default run; the full line is ``--workload corpus``."""
     from miner_amd import corpus, synthetic
@@ -1022,12 +1023,36 @@ def config5_subline(dev, steps=2, warmup=1):
     assert torch.isfinite(out[0][0]).all()
     fl = C5_U * C5_N * 4 * C5_K * D
     tflops = fl / (ms / 1e3) / 1e12
+    # one GPU's share of config 5's 1M users on 8 GPUs (125,000), ranked in one host loop
+    # (corpus.rank_corpus: 16,384 users per encode + rank pair); users shard with no data-path
+    # collective, so this is also the whole job's time at 8 GPUs
+    share = None
+    if share_users:
+        gs = torch.Generator(device=dev).manual_seed(55)
+        hs = torch.randint(0, C5_N, (share_users, C5_L), generator=gs, device=dev, dtype=torch.int32)
+        ls = torch.randint(1, C5_L + 1, (share_users,), generator=gs, device=dev)
+        ms_ = torch.arange(C5_L, device=dev)[None, :] >= (C5_L - ls)[:, None]
+        res = [None]
+
+        def share_fn():
+            res[0] = corpus.rank_corpus(table, hs, ms_, pk, C5_TOPK)
+
+        corpus.rank_corpus(table, hs[:4096], ms_[:4096], pk, C5_TOPK)      # warm-up
+        sec = _kernel_ms(share_fn, 1, 0, dev) / 1e3
+        assert torch.isfinite(res[0][0]).all()
+        share = {"users": share_users, "news": C5_N, "seconds": round(sec, 3),
+                 "value": round(share_users * C5_N / sec, 1), "unit": "(user,news) pairs/s",
+                 "what": "one GPU's share of BASELINE config 5 (1M users / 8 GPUs), encode + rank top-100 "
+                         "in batches of 16,384 users; users shard with no collective, so 8 GPUs take the "
+                         "same seconds for all 1M users"}
+        del hs, ms_, res
     return {"workload": "config 5 full-corpus ranking (2048 users x 200k news, L=200, K=64, top-100)",
             "value": round(C5_U * C5_N / (ms / 1e3), 1), "unit": "(user,news) pairs/s", "dtype": "fp16",
             "ms_per_step": round(ms, 3), "steps": steps,
             "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tflops / PEAK_BF16_TFLOPS, 4),
-                         "kernel": "ue_fused<fp16> + rk_fused<fp16> (ranker FLOPs over the whole step)"}}
+                         "kernel": "ue_fused<fp16> + rk_fused<fp16> (ranker FLOPs over the whole step)"},
+            "per_gpu_share": share}
 
 
 def run_corpus(args, rank, world, dev):

@@ -64,17 +64,18 @@ int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mu
                     int32_t* top_ids);
 
 /*
- * The same with a caller-owned device workspace of workspace_bytes bytes, sized by
- * miner_rank_topk_workspace_bytes(U, topk) (16-byte aligned; NULL: the form above). The split form
- * runs only when workspace_bytes covers it, so a workspace sized under another MINER_RK_SPLIT
- * setting is never overrun (the unsplit form runs instead). With it, on a 256-CU device and fewer than 256 two-user
- * tiles (U <= 510; MINER_RK_SPLIT=1 / 0 forces either form), the news table is split in 8 slices
- * whose per-user top-k lists are merged by a second launch (8x the workgroups for small user
- * batches), the users mapped so that the CUs of one XCD share 8 users' rows in their L2. Same
- * results as miner_rank_topk, bit for bit. miner_rank_topk_workspace_bytes returns 0 when the split
- * form would not run (larger U), so no workspace need be allocated then.
+ * The same with a caller-owned device workspace of workspace_bytes bytes (16-byte aligned; NULL: the
+ * form above). With a workspace of at least miner_rank_topk_workspace_bytes(U, topk) bytes, on a
+ * 256-CU device, the split form runs: the news table is split in 8 slices whose per-user top-k
+ * lists are merged by a second launch (8x the workgroups for small user batches), the users mapped
+ * so that the CUs of one XCD share 8 users' rows in their L2. A smaller workspace is never written
+ * (the unsplit form runs). Same results as miner_rank_topk, bit for bit.
+ * miner_rank_topk_workspace_bytes returns 0 where the split form cannot run (not a 256-CU device,
+ * invalid arguments). miner_rank_topk_split_recommended(U) is 1 where the split form is the faster
+ * one (fewer than 256 two-user tiles: U <= 510), so a caller passes a workspace only then.
  */
 size_t miner_rank_topk_workspace_bytes(int U, int topk);
+int miner_rank_topk_split_recommended(int U);
 int miner_rank_topk_ws(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
                        const void* news, int U, int N, int d, int K, int topk, float* top_scores,
                        int32_t* top_ids, void* workspace, size_t workspace_bytes);

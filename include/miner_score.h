@@ -22,13 +22,19 @@
  *   - every pointer is caller-owned DEVICE memory, row-major and contiguous, 16-byte aligned;
  *     nothing is allocated inside, nothing synchronises: work is enqueued on `stream`
  *     (a hipStream_t; NULL = the default stream) and the call returns immediately;
- *   - `dtype` selects the element type of the activation AND weight tensors
- *     (MINER_DTYPE_F32 = exact fp32 arithmetic, the parity mode; MINER_DTYPE_BF16 = bf16 operands
- *     with fp32 accumulation, the throughput mode). Masks are uint8 (0/1, torch.bool storage),
- *     offsets int32, bias/scores/user_out fp32;
+ *   - `dtype` selects the element type of the activation AND weight tensors and the arithmetic:
+ *     MINER_DTYPE_F32 = fp32 tensors, fp32-class products (the parity mode: within 1e-5 of the
+ *     reference's fp32 path; see each entry point for the form, e.g. bf16x6 on the bf16 matrix
+ *     cores for miner_score), MINER_DTYPE_F32_MFMA = the same fp32 tensors with every product on
+ *     the fp32 MFMA (exact fp32 fma chains), MINER_DTYPE_BF16 = bf16 operands with fp32
+ *     accumulation, the throughput mode. Masks are uint8 (0/1, torch.bool storage), offsets int32,
+ *     bias/scores/user_out fp32;
  *   - return 0 on success, a negative MINER_E* code for invalid arguments (nothing launched), or a
  *     positive hipError_t from the launch. miner_strerror() names the code.
- *   - no global state beyond a cached device-attribute query: thread-safe per stream.
+ *   - no global state beyond a cached device-attribute query: thread-safe per stream. The product
+ *     library reads no environment variable; every kernel form is chosen by the arguments. Two
+ *     timing-ablation switches of the diagnostic tools (MINER_NEWS_ABL: miner_score_news;
+ *     MINER_FF_ABL: miner_fastformer_score) are read once per process, 0 when unset.
  */
 #ifndef MINER_SCORE_H
 #define MINER_SCORE_H
@@ -40,10 +46,20 @@
 extern "C" {
 #endif
 
-#define MINER_ABI_VERSION 4
+#define MINER_ABI_VERSION 5
 
-/* MINER_DTYPE_F16 is accepted by the full-corpus entry points of miner_corpus.h only (config 5) */
-enum miner_dtype { MINER_DTYPE_F32 = 0, MINER_DTYPE_BF16 = 1, MINER_DTYPE_F16 = 2 };
+/* MINER_DTYPE_F16 is accepted by the full-corpus entry points of miner_corpus.h only (config 5).
+ * MINER_DTYPE_F32_MFMA (fp32 tensors, every product on the fp32 MFMA) by miner_score,
+ * miner_score_gather, miner_target_aware and the host queries of this header; MINER_DTYPE_F32_X6
+ * (fp32 tensors, news_score32's products as bf16x6 on the bf16 matrix cores) by miner_score_news
+ * and miner_news_supported (miner_news.h). */
+enum miner_dtype {
+  MINER_DTYPE_F32 = 0,
+  MINER_DTYPE_BF16 = 1,
+  MINER_DTYPE_F16 = 2,
+  MINER_DTYPE_F32_MFMA = 3,
+  MINER_DTYPE_F32_X6 = 4
+};
 
 /* src/model/model.py:128-136 ('weighted' = TargetAwareAttention). NONE = PolyAttention only. */
 enum miner_score_type {
@@ -87,8 +103,8 @@ int miner_pack_target_weights(void* stream, int dtype, const void* w_target, int
  * dtype MINER_DTYPE_F32 (the reference's precision): the W1·Eᵀ and W2·muiᵀ contractions run as
  * bf16x6 on the bf16 matrix cores (each fp32 operand cut exactly into three bf16 terms, the six
  * leading partial products, fp32 accumulation; error vs float64 within 1.5x the fp32 MFMA's), the
- * rest on the fp32 MFMA; the process environment variable MINER_DENSE_FP32=mfma32, read at each
- * call, selects every product on the fp32 MFMA (exact fp32 fma chains).
+ * rest on the fp32 MFMA. dtype MINER_DTYPE_F32_MFMA: every product on the fp32 MFMA (exact fp32
+ * fma chains; the Python layer passes it under MINER_DENSE_FP32=mfma32).
  *   history      [B, L, d]  dtype  clicked-news embeddings, left-padded (reader.py:369)
  *   his_mask     [B, L]     uint8  1 = real click, 0 = pad (entities.py:395)
  *   his_bias     [B, L]     fp32   optional category bias, already averaged over the candidates

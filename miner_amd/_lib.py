@@ -13,10 +13,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MINER_HIP_LIB", os.path.join(_HERE, "libminer_hip.so"))
 
 # enums of include/miner_score.h
-DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
+DTYPE_F32, DTYPE_BF16, DTYPE_F16, DTYPE_F32_MFMA, DTYPE_F32_X6 = 0, 1, 2, 3, 4
 SCORE_WEIGHTED, SCORE_MAX, SCORE_MEAN, SCORE_NONE = 0, 1, 2, 3
 SCORE_TYPES = {"weighted": SCORE_WEIGHTED, "max": SCORE_MAX, "mean": SCORE_MEAN, "none": SCORE_NONE}
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # every symbol include/*.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
@@ -45,6 +45,7 @@ SIGNATURES = {
     "miner_encode_users": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "miner_rank_topk": (_I, [_P, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "miner_rank_topk_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
+    "miner_rank_topk_split_recommended": (_I, [_I]),
     "miner_rank_topk_ws": (_I, [_P, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, ctypes.c_size_t]),
     # include/miner_news.h
     "miner_news_precompute": (_I, [_P, _I, _P, _I, _P, _I, _I, _I, _P, _P]),

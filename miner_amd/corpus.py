@@ -12,6 +12,7 @@ Device tensors only: there is no CPU path.
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Optional
 
 import torch
@@ -127,12 +128,41 @@ def rank_topk(user_mui: Tensor, user_proj: Optional[Tensor], news: Tensor, topk:
     dev = mui.device
     top_s = torch.empty(U, topk, dtype=torch.float32, device=dev)
     top_i = torch.empty(U, topk, dtype=torch.int32, device=dev)
-    # a workspace only when the split form will run (U <= 510 on a 256-CU device, or MINER_RK_SPLIT=1):
-    # 0 bytes otherwise, and the kernel then takes the unsplit form
-    nws = int(_lib.lib().miner_rank_topk_workspace_bytes(U, topk))
+    # a workspace only where the split form runs: the library's recommendation (U <= 510 on a 256-CU
+    # device), or MINER_RK_SPLIT=1 / 0 (read here, per call: a test / A/B switch) forcing either form
+    lib = _lib.lib()
+    force = os.environ.get("MINER_RK_SPLIT", "")
+    split = force == "1" if force in ("0", "1") else bool(lib.miner_rank_topk_split_recommended(U))
+    nws = int(lib.miner_rank_topk_workspace_bytes(U, topk)) if split else 0
     ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws else None
     with torch.cuda.device(dev):
         rc = _lib.lib().miner_rank_topk_ws(_stream(dev), dt, st, _ptr(mui), _ptr(proj), _ptr(tab), U, N, d, K, topk,
                                            _ptr(top_s), _ptr(top_i), _ptr(ws), nws)
     _lib.check(rc, "miner_rank_topk")
+    return top_s, top_i
+
+
+def rank_corpus(news: Tensor, his_ids: Tensor, his_mask: Tensor, packed: EncoderWeights, topk: int, *,
+                his_bias: Optional[Tensor] = None, score_type: str = "weighted", batch: int = 16384,
+                out: Optional[tuple] = None):
+    """BASELINE config 5 on one GPU's share of the users: every user (his_ids [U,L] into the news
+    table [N,d], his_mask [U,L]) encoded and ranked against the whole table, ``batch`` users per
+    encode + rank pair so that the [batch,K,d] user vectors are all that is ever held (125,000 users
+    at K = 64, d = 768, fp16 would be 24.6 GB of mui + proj at once). Returns (scores [U,topk] fp32,
+    ids [U,topk] int32), best first: each user's list is independent of the batching
+    (tests/test_gpu_fullsize.py). ``out`` = preallocated (scores, ids) to write into."""
+    if batch <= 0:
+        raise ValueError("batch must be positive")
+    U = his_ids.shape[0]
+    dev = news.device
+    top_s, top_i = out if out is not None else (torch.empty(U, topk, dtype=torch.float32, device=dev),
+                                                torch.empty(U, topk, dtype=torch.int32, device=dev))
+    with_proj = score_type == "weighted"
+    for u0 in range(0, U, batch):
+        u1 = min(U, u0 + batch)
+        mui, proj = encode_users(news, his_mask[u0:u1], packed, his_ids=his_ids[u0:u1],
+                                 his_bias=None if his_bias is None else his_bias[u0:u1], with_proj=with_proj)
+        s, i = rank_topk(mui, proj, news, topk, score_type=score_type)
+        top_s[u0:u1] = s
+        top_i[u0:u1] = i
     return top_s, top_i

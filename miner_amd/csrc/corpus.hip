@@ -915,31 +915,26 @@ int ue_dispatch(void* stream, const UeParams& prm) {
 // the 256 CUs its tile-to-XCD map assumes, and the users are too few to fill the CUs with 2-user
 // tiles (< 256 two-user tiles, i.e. U <= 510): at U = 2,048 it measured 90.5 vs 85.9 ms per config-5 step (each slice's
 // top-k warms up on its own; its L2 hit rate is higher, 69 vs 45 %, but the stream is not what
-// bounds it). MINER_RK_SPLIT=1 / 0 forces either form.
-// Fewer than 256 two-user tiles means U <= 510.
-bool rk_split_wanted(int U) {
-  if (num_cus() != 256) return false;
-  const char* ev = getenv("MINER_RK_SPLIT");
-  if (ev && (ev[0] == '0' || ev[0] == '1')) return ev[0] == '1';
-  return (U + kUT - 1) / kUT < num_cus();
-}
+// bounds it). The caller chooses by passing a workspace (miner_rank_topk_split_recommended says
+// which form the library would take). Fewer than 256 two-user tiles means U <= 510.
+bool rk_split_wanted(int U) { return num_cus() == 256 && (U + kUT - 1) / kUT < num_cus(); }
 size_t rk_ws_bytes(int U, int topk) { return (size_t)U * kSplit * topk * 8; }
-// the split form runs only on a workspace the caller says is large enough for it (the variable may
-// change between the size query and the launch; the launch never trusts the query's answer)
+// the split form runs only on a workspace whose stated size covers it (the launch never trusts an
+// earlier size query), on the 256-CU device its tile-to-XCD map assumes
 bool rk_split(const RkParams& prm) {
   if (prm.ws_s == nullptr || prm.ws_i == nullptr || prm.ws_bytes < rk_ws_bytes(prm.U, prm.topk)) return false;
-  return rk_split_wanted(prm.U);
+  return num_cus() == 256;
 }
 
 template <class T, int NKT, int S, int GEO>
 int rk_launch_geo(void* stream, const RkParams& prm, bool split) {
-  // d = 768 in 16-bit (config 5): the chunk count compile-time (MINER_RK_NCH_RT: the run-time form)
+  // d = 768 in 16-bit (config 5): the chunk count compile-time
   void (*kern)(RkParams) = split ? rk_fused<T, NKT, S, 0, kSplit, GEO> : rk_fused<T, NKT, S, 0, 1, GEO>;
   if constexpr (sizeof(T) == 2) {
     // config 5's d = 768 and K = 64 compile-time (the masked interest loops of the epilogue compile
     // away; the top-k equals the oracle's at the 16-bit bar, tests/test_gpu_corpus.py)
     constexpr int kN768 = 768 * 2 / kRB<GEO>;
-    if (prm.d == 768 && !getenv("MINER_RK_NCH_RT")) {
+    if (prm.d == 768) {
       if (NKT == 2 && prm.K == 64)
         kern = split ? rk_fused<T, NKT, S, kN768, kSplit, GEO, 64> : rk_fused<T, NKT, S, kN768, 1, GEO, 64>;
       else
@@ -1053,10 +1048,11 @@ int miner_encode_users(void* stream, int dtype, const void* history, const int32
 }
 
 size_t miner_rank_topk_workspace_bytes(int U, int topk) {
-  if (U <= 0 || topk <= 0 || topk > kMaxTopk) return 0;
-  if (!rk_split_wanted(U)) return 0;     // the unsplit form needs no workspace
+  if (U <= 0 || topk <= 0 || topk > kMaxTopk || num_cus() != 256) return 0;
   return rk_ws_bytes(U, topk);
 }
+
+int miner_rank_topk_split_recommended(int U) { return U > 0 && rk_split_wanted(U) ? 1 : 0; }
 
 int miner_rank_topk(void* stream, int dtype, int score_type, const void* user_mui, const void* user_proj,
                     const void* news, int U, int N, int d, int K, int topk, float* top_scores, int32_t* top_ids) {

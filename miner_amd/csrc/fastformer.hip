@@ -1173,8 +1173,9 @@ int launch(void* stream, const FfParams& prm) {
 
 int run(void* stream, int dtype, const FfParams& prm_in) {
   FfParams prm = prm_in;
-  const char* abl = getenv("MINER_FF_ABL");
-  prm.abl = abl ? atoi(abl) : 0;
+  // timing-ablation bits of the diagnostic tools (tools/ff_ab.py): read once per process
+  static const int abl = [] { const char* e = getenv("MINER_FF_ABL"); return e ? atoi(e) : 0; }();
+  prm.abl = abl;
   const bool gather = prm.his_ids != nullptr;
   if (dtype == MINER_DTYPE_BF16) return gather ? launch<__bf16, true>(stream, prm) : launch<__bf16, false>(stream, prm);
   return gather ? launch<float, true>(stream, prm) : launch<float, false>(stream, prm);

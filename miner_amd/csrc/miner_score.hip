@@ -1141,7 +1141,8 @@ Carve carve(int dtype, int mode, int L, int d, int Dc) {
   return c;
 }
 
-int check_shape(int dtype, int mode, int L, int d, int Dc, int K) {
+int check_shape(int dtype_in, int mode, int L, int d, int Dc, int K) {
+  const int dtype = dtype_in == MINER_DTYPE_F32_MFMA ? MINER_DTYPE_F32 : dtype_in;
   if (dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) return MINER_EINVAL;
   if (d <= 0 || K <= 0) return MINER_EINVAL;
   if (mode == kFull && (L <= 0 || Dc <= 0)) return MINER_EINVAL;
@@ -1178,7 +1179,13 @@ int launch(void* stream, const Params& prm, int lds) {
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
-int run(void* stream, int dtype, int mode, Params prm) {
+// MINER_DTYPE_F32_MFMA is MINER_DTYPE_F32 with every product on the fp32 MFMA (exact fp32 fma
+// chains) instead of the bf16x6 default: the same operands, layouts and carve
+int base_dtype(int dtype) { return dtype == MINER_DTYPE_F32_MFMA ? MINER_DTYPE_F32 : dtype; }
+
+int run(void* stream, int dtype_in, int mode, Params prm) {
+  const bool exact32 = dtype_in == MINER_DTYPE_F32_MFMA;
+  const int dtype = base_dtype(dtype_in);
 #ifdef MINER_STAMPS
   if (const char* e = getenv("MINER_DBG")) prm.dbg = atoi(e);
 #endif
@@ -1189,9 +1196,7 @@ int run(void* stream, int dtype, int mode, Params prm) {
   const bool gather = prm.his_ids != nullptr;
   if (dtype == MINER_DTYPE_BF16) {
     // config 3's model (d = 768, history 50, Dc = 200, K = 32), dense rows: the shape compile-time
-    // as well (MINER_SCORE_SHP_RT: the run-time form, for A/B)
-    if (prm.d == 768 && mode == kFull && !gather && prm.L == 50 && prm.Dc == 200 && prm.K == 32 &&
-        !getenv("MINER_SCORE_SHP_RT"))
+    if (prm.d == 768 && mode == kFull && !gather && prm.L == 50 && prm.Dc == 200 && prm.K == 32)
       return launch<__bf16, kFull, 24, false, 1>(stream, prm, c.total);
     // bf16 kernels specialised on the embedding dim (d = 32*NS) so the slab loops fully unroll
     switch (prm.d) {
@@ -1207,9 +1212,8 @@ int run(void* stream, int dtype, int mode, Params prm) {
         return gather ? launch<__bf16, kFull, 0, true>(stream, prm, c.total) : launch<__bf16, kFull, 0>(stream, prm, c.total);
     }
   }
-  // fp32: bf16x6 products by default, the exact fp32-MFMA form on MINER_DENSE_FP32=mfma32
-  const char* f32mode = getenv("MINER_DENSE_FP32");
-  if (f32mode && strcmp(f32mode, "mfma32") == 0) {
+  // fp32: bf16x6 products by default, the exact fp32-MFMA form for MINER_DTYPE_F32_MFMA
+  if (exact32) {
     if (mode == kTaa) return launch<float, kTaa, 0>(stream, prm, c.total);
     return gather ? launch<float, kFull, 0, true>(stream, prm, c.total) : launch<float, kFull, 0>(stream, prm, c.total);
   }
@@ -1343,7 +1347,7 @@ int miner_supported(int dtype, int L, int d, int Dc, int K) { return check_shape
 
 int miner_lds_bytes(int dtype, int score_type, int L, int d, int Dc) {
   (void)score_type;
-  return carve(dtype, kFull, L, d, Dc).total;
+  return carve(base_dtype(dtype), kFull, L, d, Dc).total;
 }
 
 const char* miner_strerror(int code) {

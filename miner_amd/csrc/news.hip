@@ -94,9 +94,6 @@ __device__ __forceinline__ float rows4_sum(float x) {
 __device__ __forceinline__ uint32_t lds_u32(const char* p) { return *reinterpret_cast<const uint32_t*>(p); }
 __device__ __forceinline__ u32x4 lds_u32x4(const char* p) { return *reinterpret_cast<const u32x4*>(p); }
 
-#ifndef NS_D256_CW128
-#define NS_D256_CW128 0
-#endif
 #ifndef NS_ABL
 #define NS_ABL 0         // timing ablations of news_score (wrong scores): 2 no row DMAs, 4 no products
 #endif
@@ -2057,7 +2054,7 @@ int num_cus() {
 inline bool aligned16(const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; }
 
 int check_news(int dtype, int L, int d, int Dc, int K) {
-  if (dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16) return MINER_EINVAL;
+  if (dtype != MINER_DTYPE_F32 && dtype != MINER_DTYPE_BF16 && dtype != MINER_DTYPE_F32_X6) return MINER_EINVAL;
   if (L <= 0 || d <= 0 || K <= 0 || Dc <= 0) return MINER_EINVAL;
   if (L > kMaxL || K > kMaxK || (K & 3) || d % 64 || d > kMaxD || Dc > kMaxDc) return MINER_ESHAPE;
   return MINER_OK;
@@ -2095,21 +2092,23 @@ int launch_pre2(void* stream, const PreParams& prm) {
 
 template <class T>
 int run_pre(void* stream, const PreParams& prm, int lds) {
-  if constexpr (sizeof(T) == 2) {
-    if (!getenv("MINER_NEWS_PRE1")) return prm.d == 768 ? launch_pre2<24>(stream, prm) : launch_pre2<0>(stream, prm);
-  }
-  switch (prm.d >> 5) {
-    case 2: return launch_pre<T, 2>(stream, prm, lds);
-    case 4: return launch_pre<T, 4>(stream, prm, lds);
-    case 8: return launch_pre<T, 8>(stream, prm, lds);
-    case 16: return launch_pre<T, 16>(stream, prm, lds);
-    case 24: return launch_pre<T, 24>(stream, prm, lds);
-    default: return launch_pre<T, 0>(stream, prm, lds);
+  if constexpr (sizeof(T) == 2) {     // bf16: the GEMM-shaped news_pre2 (round 1 v7: 0.34 -> 0.23 ms)
+    return prm.d == 768 ? launch_pre2<24>(stream, prm) : launch_pre2<0>(stream, prm);
+  } else {
+    switch (prm.d >> 5) {
+      case 2: return launch_pre<T, 2>(stream, prm, lds);
+      case 4: return launch_pre<T, 4>(stream, prm, lds);
+      case 8: return launch_pre<T, 8>(stream, prm, lds);
+      case 16: return launch_pre<T, 16>(stream, prm, lds);
+      case 24: return launch_pre<T, 24>(stream, prm, lds);
+      default: return launch_pre<T, 0>(stream, prm, lds);
+    }
   }
 }
 
+// x6: news_score32's bf16x6 form (dtype MINER_DTYPE_F32_X6) instead of the fp32-MFMA one
 template <class T>
-int launch_score(void* stream, const NsParams& prm) {
+int launch_score(void* stream, const NsParams& prm, bool x6 = false) {
   void (*kern)(NsParams) = nullptr;
   const bool rg = prm.cand_off != nullptr;
 #define NEWS_PICK_NS(PDV, CWV, NCHV, SHPV)                                                               \
@@ -2122,18 +2121,13 @@ int launch_score(void* stream, const NsParams& prm) {
 #define NEWS_PICK(PDV, CWV) NEWS_PICK_N(PDV, CWV, 0)
   if constexpr (sizeof(T) == 2) {
     const int nchunk = prm.d >> 6;
-    const bool rt = getenv("MINER_NEWS_NCH_RT") != nullptr;    // A/B: the run-time chunk count
-    const bool mind = prm.L == 50 && prm.K == 32 && !getenv("MINER_NEWS_SHP_RT");   // MIND: history 50, 32 interests
-    if (prm.d % 128 == 0 && prm.d >= 512 && !getenv("MINER_NEWS_CW64")) {
+    const bool mind = prm.L == 50 && prm.K == 32;   // MIND: history 50, 32 interests
+    if (prm.d % 128 == 0 && prm.d >= 512) {
       // config 3: compile-time chunk count (the compile-time shape measured 1.1 % slower here)
-      if (prm.d == 768 && !rt) { NEWS_PICK_N(1, 128, 6) }
+      if (prm.d == 768) { NEWS_PICK_N(1, 128, 6) }
       else { NEWS_PICK(1, 128) }       // 128-column chunks, double-buffered
-    } else if (prm.d == 256 && !rt) {  // config 2
-#if NS_D256_CW128                      // A/B: 128-column chunks (2 per row), double-buffered
-      if (mind && NS_D256_CW128 == 2) { NEWS_PICK_NS(1, 128, 2, 1) } else { NEWS_PICK_N(1, 128, 2) }
-#else
+    } else if (prm.d == 256) {         // config 2
       if (mind) { NEWS_PICK_NS(3, 64, 4, 1) } else { NEWS_PICK_N(3, 64, 4) }
-#endif
     } else if (nchunk >= 3) {
       NEWS_PICK(3, 64)
     } else if (nchunk == 2) {
@@ -2141,10 +2135,10 @@ int launch_score(void* stream, const NsParams& prm) {
     } else {
       NEWS_PICK(1, 64)
     }
-  } else if (!getenv("MINER_NEWS_F32V1")) {
-    // fp32: news_score32 (16x16x4 fp32 MFMA tiles, 32-column chunks computed in pairs)
-    // fp32: news_score32 on the fp32 matrix cores (exact fp32 fma chains); MINER_NEWS_F32X6=1 selects
-    // the bf16x6 form (same accuracy class, bf16 matrix cores; measured equal speed at config 3)
+  } else {
+    // fp32: news_score32 on the fp32 matrix cores (exact fp32 fma chains, 16x16x4 tiles, 32-column
+    // chunks computed in pairs); dtype MINER_DTYPE_F32_X6 selects the bf16x6 form (same accuracy
+    // class, bf16 matrix cores; measured equal speed at config 3)
 #define NEWS_PICK32S(X6V, NCH, SHPV)                                                                     \
     switch (prm.score_type) {                                                                            \
       case MINER_SCORE_WEIGHTED: kern = rg ? news_score32<MINER_SCORE_WEIGHTED, true, X6V, NCH, SHPV> : news_score32<MINER_SCORE_WEIGHTED, false, X6V, NCH, SHPV>; break; \
@@ -2152,15 +2146,14 @@ int launch_score(void* stream, const NsParams& prm) {
       default: kern = rg ? news_score32<MINER_SCORE_MAX, true, X6V, NCH, SHPV> : news_score32<MINER_SCORE_MAX, false, X6V, NCH, SHPV>; break; \
     }
 #define NEWS_PICK32(X6V, NCH) NEWS_PICK32S(X6V, NCH, 0)
-    const bool x6 = getenv("MINER_NEWS_F32X6") != nullptr;
-    const bool mind = prm.L == 50 && prm.K == 32 && !getenv("MINER_NEWS_SHP_RT");   // MIND: history 50, 32 interests
-    const bool plain = !prm.bias && !prm.mui_out && !getenv("MINER_NEWS_PLAIN_RT");  // no bias, no mui output
+    const bool mind = prm.L == 50 && prm.K == 32;          // MIND: history 50, 32 interests
+    const bool plain = !prm.bias && !prm.mui_out;          // no bias, no mui output
     if (prm.d == 768) {                // config 3 (MIND-large): the chunk count compile-time
       if (x6) { NEWS_PICK32(true, 24) }
       else if (mind && plain) { NEWS_PICK32S(false, 24, 2) }
       else if (mind) { NEWS_PICK32S(false, 24, 1) }
       else { NEWS_PICK32(false, 24) }
-    } else if (prm.d == 256 && !getenv("MINER_NEWS_NCH_RT")) {   // config 2 (MIND-small)
+    } else if (prm.d == 256) {         // config 2 (MIND-small)
       if (x6) { NEWS_PICK32(true, 8) }
       else if (mind && plain) { NEWS_PICK32S(false, 8, 2) }
       else if (mind) { NEWS_PICK32S(false, 8, 1) }
@@ -2170,8 +2163,6 @@ int launch_score(void* stream, const NsParams& prm) {
     }
 #undef NEWS_PICK32
 #undef NEWS_PICK32S
-  } else {
-    NEWS_PICK(1, 64)
   }
 #undef NEWS_PICK
 #undef NEWS_PICK_N
@@ -2220,7 +2211,7 @@ int miner_news_supported(int dtype, int L, int d, int Dc, int K) {
 
 int miner_news_precompute(void* stream, int dtype, const void* news_table, int n_news, const void* packed_weights,
                           int d, int Dc, int K, float* news_logits, void* news_proj) {
-  if (!news_table || !packed_weights || !news_logits || n_news <= 0) return MINER_EINVAL;
+  if (!news_table || !packed_weights || !news_logits || n_news <= 0 || dtype == MINER_DTYPE_F32_X6) return MINER_EINVAL;
   const int rc = miner_news_supported(dtype, 1, d, Dc, K);
   if (rc != MINER_OK) return rc;
   if (!aligned16(news_table) || !aligned16(packed_weights) || !aligned16(news_logits) || !aligned16(news_proj))
@@ -2247,13 +2238,16 @@ int miner_score_news(void* stream, int dtype, int score_type, const void* news_t
   }
   if (!aligned16(news_table) || !aligned16(news_logits) || !aligned16(news_proj)) return MINER_EALIGN;
   if (B == 0) return MINER_OK;
-  const char* abl = getenv("MINER_NEWS_ABL");
+  // timing-ablation bits of the diagnostic tools (tools/news_ablate.py): read once per process;
+  // news_score32 compiles them out of the product build (MINER_NEWS_ABL_MASK = 0)
+  static const int abl = [] { const char* e = getenv("MINER_NEWS_ABL"); return e ? atoi(e) : 0; }();
   NsParams prm{news_table, news_logits, news_proj, his_ids, his_mask, his_bias,
                score_type == MINER_SCORE_NONE ? nullptr : cand_ids,
                score_type == MINER_SCORE_NONE ? nullptr : cand_offsets,
                scores, user_out, n_news, B, L, score_type == MINER_SCORE_NONE ? 0 : C, d, K, score_type,
-               abl ? atoi(abl) : 0};
-  return dtype == MINER_DTYPE_BF16 ? launch_score<__bf16>(stream, prm) : launch_score<float>(stream, prm);
+               abl};
+  return dtype == MINER_DTYPE_BF16 ? launch_score<__bf16>(stream, prm)
+                                   : launch_score<float>(stream, prm, dtype == MINER_DTYPE_F32_X6);
 }
 
 }  // extern "C"

@@ -57,34 +57,17 @@
 
 namespace {
 
+// Timing ablations only (tools/x2_ab.py builds; the product build never sets it; wrong scores):
+// 2 no row DMAs, 4 no products, 8 no GELU, 16 no candidate MFMAs, 32 no history MFMAs. The
+// measured-negative variants of rounds 4-5 (the per-impression work spread over the chunks, the
+// 3-slot ring, S7 one chunk later, the dedupe on a mui wave, M0 left clobbered, two workgroups per
+// CU) are not in this file: DESIGN §6i keeps their numbers.
 #ifndef X2_ABL
-#define X2_ABL 0       // timing ablations only (wrong scores): 2 no row DMAs, 4 no products, 8 no GELU, 16 no candidate MFMAs, 32 no history MFMAs
+#define X2_ABL 0
 #endif
-#ifndef X2_SOFT_HALF
-#define X2_SOFT_HALF 1 // <= 32 history groups: the softmax over the first 32 only (the second block's A unused)
-#endif
-#ifndef X2_DMA_EARLY
-#define X2_DMA_EARLY 1 // the next chunk's row DMAs issued right after the barrier, before a pass start's S7 / softmax / aux work
-#endif
-#ifndef X2_PIPE
-#define X2_PIPE 0      // (measured +6 %, r05) the per-impression work spread over the chunks of the previous impression (compile-time chunk counts >= 4, no eval loss)
-#endif
-#ifndef X2_S7_LATE
-#define X2_S7_LATE 0   // A/B: S7 of the previous pass at a pass's second chunk instead of its first
-#endif
-#ifndef X2_DEDUPE_WAVE
-#define X2_DEDUPE_WAVE 7 // A/B: the wave that runs the dedupe (PIPE: 3)
-#endif
-#ifndef X2_M0CLOB
-#define X2_M0CLOB 0    // A/B: the row DMAs leave M0 set (declared clobbered) instead of saving / restoring it
-#endif
-#ifndef X2_RING3
-#define X2_RING3 0     // (measured +5.4 %, r05) the 3-slot ring for the MIND shape (MINER_X2_RING3=0 / 1 overrides at run time)
-#endif
-#ifndef X2_MERGE_EARLY
-#define X2_MERGE_EARLY 1 // the dedupe's unit merge right after a barrier, before the chunk's row DMAs are issued (its compiler wait then costs nothing)
-#endif
-constexpr int kNB = 2;                                 // row-DMA blocks per wave per part
+// (eval-loss form, GS: 64 no diagonal Gram tile, 128 no operand exchange / off-diagonal tile, 256 no
+// per-chunk Gram work, 512 no per-impression D step)
+constexpr int kNB = 2;                                // row-DMA blocks per wave per part
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kMaxL = 64;
@@ -122,56 +105,30 @@ constexpr int kDupB = 16;
 constexpr int kX2Lds = kOffDup + 4 * kDupB;
 static_assert(kX2Lds <= 160 * 1024, "news_score_x2 LDS");
 
-// The carve as a function of the ring depth. R3 (X2_RING3, the MIND shape with dense candidates,
-// at most 48 per impression): three slots, two chunks in flight — history parts of 52 rows (<= 50
-// groups in 4-row DMA blocks; an MFMA block's reads past them land on the next part's finite rows,
-// times an attention weight 0), 3 candidate tiles, pass partials of 48 candidates, logit blocks of
-// 56 rows, no bias / Gram; the dedupe's row units and S7's candidate units come by LDS-DMA (no load
-// the compiler can see, so none of its vmcnt waits can drain the chunk in flight).
-template <bool R3> struct X2C {
-  static constexpr int kHisRows = R3 ? 52 : 64;
-  static constexpr int kCTiles = R3 ? 3 : 4;
-  static constexpr int kPart = kHisRows * kRB;
-  static constexpr int kCPart = kCTiles * kCTile;
-  static constexpr int kSlot = 2 * kPart + kCPart;
-  static constexpr int kNSlot = R3 ? 3 : 2;
-  static constexpr int kRing = kNSlot * kSlot;
-  static constexpr int kFBlk = (R3 ? 48 : 64) * 32;    // floats of one F[P][ch] block
+// The carve by field (the names the kernel reads through Cv::)
+struct X2C {
+  static constexpr int kPart = 64 * kRB;                 // 64 history rows of a part
+  static constexpr int kSlot = 2 * kPart + 4 * kCTile;   // E[his] | proj[his] | 4 candidate tiles
+  static constexpr int kRing = 2 * kSlot;
+  static constexpr int kFBlk = 64 * 32;                  // floats of one F[P][ch] block
   static constexpr int kOffF = kRing;
-  static constexpr int kLogB = (R3 ? 56 : 64) * 128;
+  static constexpr int kLogB = 64 * 128;
   static constexpr int kOffLog = kOffF + 4 * kFBlk * 4;
-  static constexpr int kL1Cand = R3 ? 512 : 768;
-  static constexpr int kL1Unit = 768;                   // R3: the slots' E units | proj units
-  static constexpr int kL1B = R3 ? 768 + 512 : 4 * 64 * 3 + 4 * kMaxCand;
+  static constexpr int kL1Cand = 768;
+  static constexpr int kL1B = 4 * 64 * 3 + 4 * kMaxCand;
   static constexpr int kOffL1 = kOffLog + 2 * kLogB;
   static constexpr int kOffL0 = kOffL1 + 4 * kL1B;
   static constexpr int kOffPrep = kOffL0 + 8 * kL0B;
   static constexpr int kOffGram = kOffPrep + 3 * kPrepB;
-  static constexpr int kOffDup = kOffGram + (R3 ? 0 : kGramB);
-  static constexpr int kOffUc = kOffDup + 4 * kDupB;    // R3: S7's candidate units, 64 floats
-  static constexpr int kLds = kOffUc + (R3 ? 512 : 0);   // two buffers of 64
+  static constexpr int kOffDup = kOffGram + kGramB;
+  static constexpr int kLds = kOffDup + 4 * kDupB;
 };
-static_assert(X2C<false>::kLds == kX2Lds, "x2 carve");
-static_assert(X2C<true>::kLds <= 160 * 1024, "x2 R3 carve");
+static_assert(X2C::kLds == kX2Lds, "x2 carve");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-// wait until at most n (wave-uniform, 0..7) of this wave's vector-memory operations are in flight
-__device__ __forceinline__ void vm_wait_n(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-  }
-}
-
 __device__ __forceinline__ float x_both_max(float x) {
   const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
@@ -192,11 +149,6 @@ __device__ __forceinline__ float x_rows4_sum(float x) {
 
 // one row DMA (saddr form: scalar base + 32-bit per-lane offset) into M0 = m, M0 saved / restored
 __device__ __forceinline__ void x2_dma_row(uint32_t off, const char* base, unsigned m) {
-#if X2_M0CLOB
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-               :: "v"(off), "s"(base), "s"(__builtin_amdgcn_readfirstlane(m)) : "memory", "m0");
-  return;
-#endif
   unsigned t;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
                "s_mov_b32 m0, %0"
@@ -380,14 +332,13 @@ struct X2Params {
   int n_news, B, L, C, d, K, score_type;
 };
 
-template <bool R3> __device__ __forceinline__ int* l1_his(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B); }
-template <bool R3> __device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return reinterpret_cast<uint32_t*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + 256); }
-template <bool R3> __device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + 512); }
-template <bool R3> __device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + X2C<R3>::kL1Cand); }
-template <bool R3> __device__ __forceinline__ float* l1_unit(char* smem, int slot) { return reinterpret_cast<float*>(smem + X2C<R3>::kOffL1 + slot * X2C<R3>::kL1B + X2C<R3>::kL1Unit); }
-template <bool R3> __device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffL0 + slot * kL0B); }
-template <bool R3> __device__ __forceinline__ int* dup_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C<R3>::kOffDup + slot * kDupB); }
-template <bool R3> __device__ __forceinline__ float* prep_blk(char* smem, int i) { return reinterpret_cast<float*>(smem + X2C<R3>::kOffPrep + (i % 3) * kPrepB); }
+__device__ __forceinline__ int* l1_his(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C::kOffL1 + slot * X2C::kL1B); }
+__device__ __forceinline__ uint32_t* l1_mask(char* smem, int slot) { return reinterpret_cast<uint32_t*>(smem + X2C::kOffL1 + slot * X2C::kL1B + 256); }
+__device__ __forceinline__ float* l1_bias(char* smem, int slot) { return reinterpret_cast<float*>(smem + X2C::kOffL1 + slot * X2C::kL1B + 512); }
+__device__ __forceinline__ int* l1_cand(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C::kOffL1 + slot * X2C::kL1B + X2C::kL1Cand); }
+__device__ __forceinline__ int* l0_off(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C::kOffL0 + slot * kL0B); }
+__device__ __forceinline__ int* dup_u(char* smem, int slot) { return reinterpret_cast<int*>(smem + X2C::kOffDup + slot * kDupB); }
+__device__ __forceinline__ float* prep_blk(char* smem, int i) { return reinterpret_cast<float*>(smem + X2C::kOffPrep + (i % 3) * kPrepB); }
 
 // NCH: 64-column chunks per row (0: d / 64 at run time). SHP 2: the MIND shape (history L = 50,
 // K = 32 interests) compile-time, no category bias and no mui output (plain scoring: the bench, the
@@ -397,7 +348,7 @@ template <bool R3> __device__ __forceinline__ float* prep_blk(char* smem, int i)
 // for both interest tiles (the transposed E reads are shared) and add the 3 Gram tiles of their 32
 // columns; at the pass end wave 2 hands its tiles to wave 0 through LDS, which forms D at the next
 // chunk (no mui is written).
-template <int ST, bool RAGGED, int NCH, int SHP, bool LOSS = false, bool R3 = false>
+template <int ST, bool RAGGED, int NCH, int SHP, bool LOSS = false>
 __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
@@ -411,27 +362,23 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   const float* const bias = SHP == 2 ? nullptr : p.bias;
   float* const mui_out = SHP == 2 ? nullptr : p.mui_out;
   float* const dis_out = LOSS ? p.dis_out : nullptr;
-  // PIPE: impression ci's per-impression work runs spread over the chunks of pass 0 of impression
-  // ci - 1 (schedule below), so no chunk carries all of it and the row stream keeps flowing; the
-  // dedupe then moves to a mui wave (the X waves run S7)
-  using Cv = X2C<R3>;
-  static_assert(!R3 || (SHP == 2 && !RAGGED && !LOSS && NCH >= 2), "the 3-slot ring: MIND shape, dense, no eval loss");
-  // ring slot of chunk t (the kernel-wide chunk counter): t & 1, or t % 3 kept as a rotating index
-  auto slot_of = [&](int tt) { return R3 ? tt % 3 : (tt & 1); };
-  constexpr bool PIPE = X2_PIPE && !LOSS && NCH >= 4 && !R3;
-  constexpr int kDedupeWave = PIPE ? 3 : X2_DEDUPE_WAVE;
-  constexpr bool S7LATE = X2_S7_LATE && !PIPE && !LOSS && NCH >= 3;
-  constexpr int cS7 = 1;                               // S7 of the previous pass (X waves), every pass
-  constexpr int cDED = NCH >= 8 ? 2 : 1;               // unit merge + dedupe of ci + 2 (wave 3), L0 / L1 aux DMAs
-  constexpr int cL2 = cDED + 1;                        // logit rows of ci + 2 (after its dedupe)
-  constexpr int cSM0 = NCH >= 8 ? cL2 + 1 : cL2;       // softmax of ci + 1, mui waves (after ci + 1's unit merge at cDED)
-  constexpr int cSM1 = NCH >= 8 ? cSM0 + 2 : NCH - 1;  // softmax of ci + 1, X waves
-  static_assert(!PIPE || (cSM0 > cDED && cSM1 > cDED && cSM1 < NCH && cS7 < NCH - 1), "x2 chunk schedule");
+  using Cv = X2C;
+  constexpr int kDedupeWave = 7;                       // an X wave (they wait at the barriers)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = wave >> 2, ch = (wave >> 1) & 1, kt = wave & 1;
   const bool k_live = 16 * kt < KK;
   const bool path_live = P == 0 || WEIGHTED;
-  const bool gram_w = LOSS && P == 0 && kt == 0;         // waves 0 and 2: the Gram of their 32 columns
+  // The eval loss's Gram. GS (the MIND shape: L = 50, 4 or 12 chunks): spread over the four mui
+  // waves — each adds its own diagonal 16x16 tile over its 32 columns from the operand of its
+  // candidate product (no extra split); the off-diagonal tile goes to the interest-tile-0 waves,
+  // which get the tile-1 operand of the same columns through LDS one chunk later (rows 56..63 of
+  // part ch of that chunk's ring slot: no DMA writes them at L <= 52, and the history product reads
+  // them times an attention weight of exactly 0, so only their finiteness matters). Otherwise (run-
+  // time shapes) waves 0 and 2 run the history product for both interest tiles and add all three
+  // tiles of their 32 columns.
+  constexpr bool GS = LOSS && SHP == 2;
+  static_assert(!GS || (NCH >= 3 && WEIGHTED), "the spread Gram: chunk counts >= 3, 'weighted' scoring");
+  const bool gram_w = LOSS && P == 0 && (GS || kt == 0);
   const char* tabB = static_cast<const char*>(p.table2);
   const char* prjB = WEIGHTED ? static_cast<const char*>(p.proj2) : tabB;
   const unsigned sbase = __builtin_amdgcn_readfirstlane(lds_offset(smem));
@@ -443,13 +390,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // candidate's unit for S7) and 1 / κ_k for the mui output. Set per impression.
   float kap = kSA;                         // κ_k of this lane's interest (the wave's path), per impression
   float uc_pend_r = 1.0f;                  // S7 lane's candidate unit (X waves), loaded a chunk ahead
-  int pend_ub = 0, pass_ctr = 0;           // R3: the candidate units' LDS buffer of the pending pass / this pass
 
   auto imp_b = [&](int i) { return (int)blockIdx.x + i * G; };
   auto cands = [&](int i, int& off, int& cnt) {
     if constexpr (!WITH_CAND) { off = 0; cnt = 0; return; }
     if constexpr (RAGGED) {
-      const int* o = l0_off<R3>(smem, i & 7);
+      const int* o = l0_off(smem, i & 7);
       off = __builtin_amdgcn_readfirstlane(o[0]);
       cnt = __builtin_amdgcn_readfirstlane(o[1]) - off;
     } else {
@@ -475,7 +421,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       const uintptr_t a = reinterpret_cast<uintptr_t>(p.mask + base) & ~(uintptr_t)3;
       dma_b32(reinterpret_cast<const void*>(a), l1 + 256);
     } else if (wave == 3) {
-      if (bias && !R3) dma_b32(bias + base, l1 + 512);
+      if (bias) dma_b32(bias + base, l1 + 512);
     } else if (WITH_CAND && wave >= 4) {                 // candidate ids, 64 per DMA
       int off, cnt;
       cands(i, off, cnt);
@@ -487,12 +433,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   };
   // logit rows of impression i by UNIQUE history row (after its dedupe, below)
   auto issue_L2 = [&](int i) {
-    if (i >= n_i || (R3 && wave == 7)) return;     // R3: 56 staged rows (<= 50 groups)
+    if (i >= n_i) return;
     const int lane = threadIdx.x & 63;
-    const int U = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, i & 3)[0]);
+    const int U = __builtin_amdgcn_readfirstlane(dup_u(smem, i & 3)[0]);
     const int row = min(8 * wave + (lane >> 3), U - 1);
     const int piece = min(lane & 7, (KK >> 2) - 1);
-    const int id = min(max(l1_his<R3>(smem, i & 3)[row], 0), p.n_news - 1);
+    const int id = min(max(l1_his(smem, i & 3)[row], 0), p.n_news - 1);
     x2_dma_b128(p.logits + (size_t)id * KK + 4 * piece, sbase + Cv::kOffLog + (i & 1) * Cv::kLogB + wave * 1024);
   };
   // The masked history slots holding the same news id — the left padding: every pad slot is the pad
@@ -509,17 +455,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   float du_E = 1.f, du_P = 1.f;
   int du_slot = -1, du_i = -1;
   // the merge of the pending units: the compiler waits for their loads here (vmcnt), so it is called
-  // right after a barrier (X2_MERGE_EARLY), when this wave's row DMAs have all landed, not behind the
-  // chunk DMAs it has just issued
+  // right after a barrier, when this wave's row DMAs have all landed, not behind the chunk DMAs it
+  // has just issued
   auto dedupe_merge = [&]() {
     if (wave != kDedupeWave) return;
     if (du_i >= 0) {
-      int* pcp = reinterpret_cast<int*>(prep_blk<R3>(smem, du_i));
-      if constexpr (R3) {
-        const int l = threadIdx.x & 63;
-        du_E = l1_unit<R3>(smem, du_i & 3)[l];
-        du_P = WEIGHTED ? l1_unit<R3>(smem, du_i & 3)[64 + l] : 1.0f;
-      }
+      int* pcp = reinterpret_cast<int*>(prep_blk(smem, du_i));
       if (du_slot >= 0)
         pcp[du_slot] |= (((__float_as_int(du_E) >> 23) & 255) << 8) | (((__float_as_int(du_P) >> 23) & 255) << 16);
       du_i = -1;
@@ -530,22 +471,16 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int l = threadIdx.x & 63;
     dedupe_merge();
     if (i >= n_i) return;
-    int* his = l1_his<R3>(smem, i & 3);
+    int* his = l1_his(smem, i & 3);
     const int ls = min(l, L - 1);
     const int id = his[ls];
     const int idc = min(max(id, 0), p.n_news - 1);
-    if constexpr (R3) {                  // the units by LDS-DMA (read at the merge, an impression later)
-      const unsigned ub = sbase + (unsigned)((char*)l1_unit<R3>(smem, i & 3) - smem);
-      dma_b32(p.unit_t + idc, ub);
-      if (WEIGHTED) dma_b32(p.unit_p + idc, ub + 256);
-    } else {
-      du_E = p.unit_t[idc];
-      du_P = WEIGHTED ? p.unit_p[idc] : 1.0f;
-    }
-    const uint32_t mw = l1_mask<R3>(smem, i & 3)[ls];
+    du_E = p.unit_t[idc];
+    du_P = WEIGHTED ? p.unit_p[idc] : 1.0f;
+    const uint32_t mw = l1_mask(smem, i & 3)[ls];
     const int a = (int)(reinterpret_cast<uintptr_t>(p.mask + (size_t)imp_b(i) * L + ls) & 3);
     const bool keep = ((mw >> (8 * a)) & 0xffu) != 0u;
-    const float bv = (keep && bias) ? l1_bias<R3>(smem, i & 3)[ls] : 0.f;
+    const float bv = (keep && bias) ? l1_bias(smem, i & 3)[ls] : 0.f;
     // the group: the masked slots holding the first masked slot's news id (a masked slot's logit and
     // bias never enter its score, model.py:176-180); every other slot is a group of its own
     const unsigned long long pads = __ballot(l < L && !keep);
@@ -557,7 +492,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const unsigned long long bal = __ballot(uniq);
     const int U = __popcll(bal);
     const int uidx = __popcll(bal & ((1ull << l) - 1ull));
-    float* pr = prep_blk<R3>(smem, i);
+    float* pr = prep_blk(smem, i);
     // (code, add) per group; code, an integer: bits 0-7 the multiplicity m, 8-15 / 16-23 the
     // exponent fields of the E / proj rows' units (powers of two; or'ed in by the next call), bit
     // 24 set for a click
@@ -571,7 +506,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       pc[l] = (113 << 8) | (113 << 16);  // m = 0, units 2^-14
       pr[64 + l] = -INFINITY;
     }
-    if (l == 0) dup_u<R3>(smem, i & 3)[0] = U;
+    if (l == 0) dup_u(smem, i & 3)[0] = U;
     du_slot = uniq ? uidx : -1;
     du_i = i;
   };
@@ -588,7 +523,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     int off = 0, cnt = 1;
     if (live) cands(i, off, cnt);
     const int cntp = max(1, min(64, cnt - 64 * pass));
-    const int U = live ? __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, i & 3)[0]) : 1;
+    const int U = live ? __builtin_amdgcn_readfirstlane(dup_u(smem, i & 3)[0]) : 1;
     lv = 0;
 #pragma unroll
     for (int jj = 0; jj < kNB; ++jj) {
@@ -599,8 +534,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       const uint32_t poff = (uint32_t)(((lane & 15) ^ x2swz(row)) << 4);
       int h = 0, c = 0;
       if (live) {
-        if (dmaE || dmaP) h = l1_his<R3>(smem, i & 3)[min(row, U - 1)];
-        if (dmaC) c = l1_cand<R3>(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
+        if (dmaE || dmaP) h = l1_his(smem, i & 3)[min(row, U - 1)];
+        if (dmaC) c = l1_cand(smem, i & 3)[min(64 * pass + min(row, cntp - 1), kMaxCand - 1)];
       }
       h = min(max(h, 0), p.n_news - 1);
       c = min(max(c, 0), p.n_news - 1);
@@ -610,10 +545,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     }
     lv = __builtin_amdgcn_readfirstlane(lv);
   };
-  // returns the number of row DMAs this wave issued (wave-uniform): the ring-3 wait keeps them in flight
-  auto dma_chunk = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int cc, int slot) -> int {
-    if (lv == 0 || (X2_ABL & 2)) return 0;
-    int n = 0;
+  auto dma_chunk = [&](const uint32_t* oH, const uint32_t* oC, unsigned lv, int cc, int slot) {
+    if (lv == 0 || (X2_ABL & 2)) return;
     const char* bE = tabB + cc * kRB;
     const char* bP = prjB + cc * kRB;
 #pragma unroll
@@ -622,14 +555,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       if (lv & (1u << jj)) {
         if (dmaE) x2_dma_row(oH[jj], bE, m);
         if (dmaP) x2_dma_row(oH[jj], bP, m + Cv::kPart);
-        n += (dmaE ? 1 : 0) + (dmaP ? 1 : 0);
       }
-      if (lv & (16u << jj)) {
-        x2_dma_row(oC[jj], bE, m + 2 * Cv::kPart + (dma_block(jj) >> 2) * 16);
-        ++n;
-      }
+      if (lv & (16u << jj)) x2_dma_row(oC[jj], bE, m + 2 * Cv::kPart + (dma_block(jj) >> 2) * 16);
     }
-    return n;
   };
 
   // ---- per-lane LDS read offsets (fixed for the launch) ----
@@ -660,9 +588,6 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // Aᵀ B operand of the history product, fp16 pairs: lane (g, i) holds A[16 kt + i][u] of the history
   // groups u = 32 kb + 16 (e >> 2) + 4g + (e & 3) (aH1 / aL1: interest tile 1, the Gram waves only)
   u32x4 aH[2], aL[2], aH1[2], aL1[2];
-  u32x4 aHn[2], aLn[2];                    // PIPE: the next impression's, computed a few chunks ahead
-  float kapn = kSA;
-  int nkb_n = 2;
 
   // softmax over the history groups (model.py:176-181) of this wave's 16 interests, in registers:
   // lane (g, i) takes 16 groups, the 4 lane rows combined by permlanes
@@ -673,7 +598,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     const int j = lane & 15, g = lane >> 4;
     const int k = 16 * ktile + j;
     const float* lgb = reinterpret_cast<const float*>(smem + Cv::kOffLog + (i & 1) * Cv::kLogB);
-    const float* pr = prep_blk<R3>(smem, i);
+    const float* pr = prep_blk(smem, i);
     const int* pc = reinterpret_cast<const int*>(pr);
     const unsigned sh = pth ? 16u : 8u;
     float v[NSS], wm[NSS], un[NSS];
@@ -725,7 +650,6 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   vm_wait_all();
   raw_barrier();
   dedupe_prep(0);
-  if (R3) vm_wait_all();               // impression 0's units (LDS-DMA) landed before dedupe_prep(1) merges them
   dedupe_prep(1);
   raw_barrier();
   issue_L2(0); issue_L2(1);
@@ -737,8 +661,6 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   unsigned cLv = 0, nLv = 0;
   item_offsets(0, 0, cH, cC, cLv);
   dma_chunk(cH, cC, cLv, 0, 0);
-  int n_ahead = 0;                               // R3: row DMAs of the chunk one ahead, still in flight
-  if constexpr (R3) n_ahead = dma_chunk(cH, cC, cLv, 1, 1);
 
   f32x4 acc[4];                                  // this wave's M / Lg partials, candidate tiles 0..3
 #pragma unroll
@@ -749,6 +671,8 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 #pragma unroll
   for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   int pend_d = -1;                               // impression whose D is formed at the next chunk (wave 0)
+  u32x4 gpH = u32x4{0u, 0u, 0u, 0u}, gpL = gpH;   // GS, tile-0 waves: this wave's operand of the last chunk
+  int gs_step = 0, gs_b = 0;                     // GS (kernel-uniform): D of impression gs_b, step 1 / 2 pending
   int nkb = 2;                                   // 32-row blocks of unique history rows of the item
   bool d_pending = false;                        // wave-uniform: a Gram hand-off is waiting
   X2_STAMP_DECL
@@ -787,16 +711,95 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
+  // GS. The exchange block of chunk tt's tile-1 operand of column half ch: [hi 64 lanes x 16 B | lo]
+  auto gs_xbuf = [&](int tt) { return smem + (tt & 1) * Cv::kSlot + ch * Cv::kPart + 56 * kRB; };
+  // the tile-1 operand of the chunk before (tile-0 waves), read right after each chunk's barrier
+  // and used at the end of its products (the off-diagonal tile (0, 1) with this wave's own operand
+  // of that chunk, gpH / gpL) or by the D step: its LDS latency hides behind the chunk's work
+  u32x4 gxH = u32x4{0u, 0u, 0u, 0u}, gxL = gxH;
+  auto gs_read = [&]() {
+    if (X2_ABL & (128 | 256)) return;
+    const char* xb = gs_xbuf(t - 1) + 16 * (threadIdx.x & 63);
+    gxH = *reinterpret_cast<const u32x4*>(xb);
+    gxL = *reinterpret_cast<const u32x4*>(xb + 1024);
+  };
+  auto gs_offdiag = [&]() {
+    if (X2_ABL & (128 | 256)) return;
+    gr[1] = mfma_x2(gr[1], gpH, gpL, gxH, gxL);
+  };
+  // per chunk of a Gram pass, after the operand split (mui waves): the diagonal tile; the tile-0
+  // waves take the previous chunk's off-diagonal tile and keep their operand for the next; the
+  // tile-1 waves publish theirs — a non-finite one as zeros: the block is read by the history
+  // products times 0, and the wave's own diagonal tile already carries it into the norms, so D
+  // stays NaN / inf as the reference's. (Round 6 A/B, tools/x2_ab.py: the same code on every mui
+  // wave — the tile-1 waves' off-diagonal products on zeros, to avoid moving register tuples
+  // between branches — measured +2.6 %.)
+  auto gs_chunk = [&](int cc, const float* x, const u32x4& bH, const u32x4& bL) {
+    if (X2_ABL & 256) return;
+    if (!(X2_ABL & 64)) gr[0] = mfma_x2(gr[0], bH, bL, bH, bL);
+    if (X2_ABL & 128) return;
+    if (kt == 0) {
+      if (cc > 0) gs_offdiag();
+      gpH = bH;
+      gpL = bL;
+    } else {
+      // |x| < 2^14 when finite, so the sum of the 8 is finite exactly when all 8 are
+      const float sx = ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
+      const bool fin = __builtin_isfinite(sx);
+      char* xb = gs_xbuf(t) + 16 * (threadIdx.x & 63);
+      *reinterpret_cast<u32x4*>(xb) = fin ? bH : u32x4{0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(xb + 1024) = fin ? bL : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  // step 1 (the chunk after a Gram pass, after its barrier; mui waves): the last off-diagonal tile,
+  // the norms n_k = sqrt(G_kk) from the four waves' diagonal partials (LDS [ch][kt][16], written at
+  // the pass end), this wave's share Σ G_kk' / (n_k n_k') over its tiles (k != k', (0, 1) twice) ->
+  // LDS; step 2 (a chunk later, wave 0): D = (Σ of the four shares) / K²
+  auto gs_step1 = [&]() {
+    if (P != 0 || (X2_ABL & 512)) return;
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, g = lane >> 4;
+    if (kt == 0) gs_offdiag();
+    // 1 / n_k = rsq(G_kk) (rsq(inf) = 0 and rsq(0) = inf keep a non-finite or zero mui NaN in D,
+    // as the reference's cosines); lane (g, j) needs rows m = 4g..4g+3 of its tile and column j
+    const float* gdg = reinterpret_cast<const float*>(smem + Cv::kOffGram);
+    const f32x4 dm0 = *reinterpret_cast<const f32x4*>(gdg + kt * 16 + 4 * g);
+    const f32x4 dm1 = *reinterpret_cast<const f32x4*>(gdg + 32 + kt * 16 + 4 * g);
+    const float rj = __builtin_amdgcn_rsqf(gdg[kt * 16 + j] + gdg[32 + kt * 16 + j]);
+    const float rj1 = __builtin_amdgcn_rsqf(gdg[16 + j] + gdg[48 + j]);
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float rm = __builtin_amdgcn_rsqf(dm0[e] + dm1[e]);
+      if (4 * g + e != j) sum = __builtin_fmaf(gr[0][e] * rm, rj, sum);
+      if (kt == 0) sum = __builtin_fmaf(2.0f * gr[1][e] * rm, rj1, sum);
+    }
+    // over the 16 lanes of a row (DPP row rotations), then the 4 rows (permlane swaps)
+    sum += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sum), 0x128, 0xf, 0xf, false));
+    sum += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sum), 0x124, 0xf, 0xf, false));
+    sum += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sum), 0x122, 0xf, 0xf, false));
+    sum += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sum), 0x121, 0xf, 0xf, false));
+    sum = x_rows4_sum(sum);
+    if (lane == 0) reinterpret_cast<float*>(smem + Cv::kOffGram + 256)[wave] = sum;
+    gr[0] = gr[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto gs_step2 = [&]() {
+    if (wave == 0 && (threadIdx.x & 63) == 0) {
+      const float* sh = reinterpret_cast<const float*>(smem + Cv::kOffGram + 256);
+      dis_out[gs_b] = ((sh[0] + sh[1]) + (sh[2] + sh[3])) / (float)(KK * KK);
+    }
+  };
+
   // S7 (model.py:128-136, :213-214) on the X waves 4-7: wave w candidates [16 (w - 4), +16) of the
   // finished pass, lane (kq, c) interests [8 kq, 8 kq + 8); the two column-half partials summed
   // here (ch 0 + ch 1), the 4 lane rows combined by permlanes
   auto s7 = [&]() {
-    if (wave < 4 || (R3 && wave == 7)) return;          // R3: <= 48 candidates, waves 4-6
+    if (wave < 4) return;
     const int lane = threadIdx.x & 63;
     const int cl = lane & 15, kq = lane >> 4;
     const int c = 16 * (wave & 3) + cl;
     const float* F = reinterpret_cast<const float*>(smem + Cv::kOffF);
-    const float uc_pend = R3 ? reinterpret_cast<const float*>(smem + Cv::kOffUc)[64 * pend_ub + c] : uc_pend_r;
+    const float uc_pend = uc_pend_r;
     const int sw = (c >> 1) & 31;
     float lg[8], m[8];
 #pragma unroll
@@ -846,7 +849,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     constexpr int NT = decltype(nt_c)::value;
     FRESH_LANE_IDS();
     const int g = lane >> 4, i = lane & 15;
-    const char* slot = smem + slot_of(t) * Cv::kSlot;
+    const char* slot = smem + (t & 1) * Cv::kSlot;
     const char* part = slot + P * Cv::kPart;
     f32x4 hx[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     [[maybe_unused]] f32x4 hy[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -865,13 +868,13 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       for (int ctl = 0; ctl < 2; ++ctl)
         hx[ctl] = (X2_ABL & 32) ? f32x4{__uint_as_float(eH[ctl][0] ^ aH[kb][0]), __uint_as_float(eL[ctl][1] ^ aL[kb][1]), 0.f, 0.f}
                                 : mfma_x2(hx[ctl], eH[ctl], eL[ctl], aH[kb], aL[kb]);
-      if (LOSS && (mode & 8)) {
+      if (LOSS && !GS && (mode & 8)) {
 #pragma unroll
         for (int ctl = 0; ctl < 2; ++ctl) hy[ctl] = mfma_x2(hy[ctl], eH[ctl], eL[ctl], aH1[kb], aL1[kb]);
       }
     }
     X2_STAMP(4);
-    if (LOSS && (mode & 8)) {
+    if (LOSS && !GS && (mode & 8)) {
       // Gram tiles over this wave's 32 columns: the operands of the candidate product's B side
       // (lane (g, i): columns 4g..4g+3 of both column tiles, interest i) serve as A (rows = k) and B
       float y0[8], y1[8];
@@ -929,6 +932,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
       u32x4 bH, bL;
       split8h(x, bH, bL);
+      if (GS && (mode & 8)) gs_chunk(cc, x, bH, bL);
       X2_STAMP(5);
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
@@ -950,21 +954,13 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     else compute_t(ci, cc, mode, integral_constant<int, 1>{});
   };
 
-  if constexpr (PIPE) {                          // impression 0's attention weights (the rest: a chunk schedule ahead)
-    using std::integral_constant;
-    if (n_i > 0) {
-      const int nkb0 = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, 0)[0]) > 32 ? 2 : 1;
-      if (X2_SOFT_HALF && nkb0 == 1) softmax_inwave(0, kt, P, aH, aL, kap, integral_constant<int, 8>{});
-      else softmax_inwave(0, kt, P, aH, aL, kap, integral_constant<int, 16>{});
-    }
-  }
   // static priority for the X waves 4-7 (the GELU chain)
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   for (int ci = 0; ci < n_i; ++ci) {
     int c_off, c_cnt;
     cands(ci, c_off, c_cnt);
     const int cn = max(1, (c_cnt + 63) >> 6);
-    nkb = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, ci & 3)[0]) > 32 ? 2 : 1;
+    nkb = __builtin_amdgcn_readfirstlane(dup_u(smem, ci & 3)[0]) > 32 ? 2 : 1;
     for (int cp = 0; cp < cn; ++cp) {
       const int cntp = min(64, c_cnt - 64 * cp);
       const int ntile = (max(cntp, 1) + 15) >> 4;
@@ -977,85 +973,39 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       bool did_s7 = false;
       for (int cc = 0; cc < nchunk; ++cc, ++t) {
         X2_STAMP(7);
-        // this chunk's rows (and every older DMA) landed for this wave (R3: the next chunk's stay in
-        // flight — they are the n_ahead youngest, or younger operations force part of them), then
-        // for every wave; the slot of the last chunk is free
-        if constexpr (R3) vm_wait_n(n_ahead);
-        else vm_wait_all();
+        // this chunk's rows (and every older DMA) landed for this wave, then for every wave; the
+        // slot of the last chunk is free
+        vm_wait_all();
         X2_STAMP(0);
         raw_barrier();
         X2_STAMP(1);
-        auto issue_next = [&]() {
-          if constexpr (R3) {          // two chunks ahead, into the slot chunk cc - 1 just left
-            if (cc + 2 < nchunk) {
-              n_ahead = dma_chunk(cH, cC, cLv, cc + 2, slot_of(t + 2));
-            } else {
-              if (cc + 2 == nchunk) item_offsets(ni, np, nH, nC, nLv);
-              n_ahead = dma_chunk(nH, nC, nLv, cc + 2 - nchunk, slot_of(t + 2));
-            }
-          } else if (cc + 1 < nchunk) {
-            dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
-          } else {
-            item_offsets(ni, np, nH, nC, nLv);
-            dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
-          }
-        };
         // the unit merge waits (compiler vmcnt) for the loads of the previous dedupe: here, before
         // this chunk's DMAs are issued, they have landed and the wait is free
-        if (X2_MERGE_EARLY && (!LOSS || SHP == 2) && cp == 0 && cc == (PIPE ? cDED : 0)) dedupe_merge();
-        if (X2_DMA_EARLY) issue_next();
-        if constexpr (PIPE) {
-          if (cc == 0) {
-            if (cp == 0 && ci > 0) {       // the A fragments of this impression, computed during the last
-#pragma unroll
-              for (int kb = 0; kb < 2; ++kb) {
-                aH[kb] = aHn[kb];
-                aL[kb] = aLn[kb];
-              }
-              kap = kapn;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-          if (cc == cS7) {
-            if (WITH_CAND && pend_off >= 0) s7();
-            pend_off = -1;
-          }
-          if (cp == 0) {
-            if (cc == cDED) {
-              dedupe_prep(ci + 2);         // L1 of ci + 2 landed; its logit rows are DMA'd by group next
-              issue_L0(ci + 4);
-              issue_L1(ci + 3);
-            }
-            if (cc == cL2) issue_L2(ci + 2);   // into the block impression ci's logits were read from
-            if (((cc == cSM0 && P == 0) || (cc == cSM1 && P == 1)) && ci + 1 < n_i) {
-              using std::integral_constant;
-              nkb_n = __builtin_amdgcn_readfirstlane(dup_u<R3>(smem, (ci + 1) & 3)[0]) > 32 ? 2 : 1;
-              if (X2_SOFT_HALF && nkb_n == 1) softmax_inwave(ci + 1, kt, P, aHn, aLn, kapn, integral_constant<int, 8>{});
-              else softmax_inwave(ci + 1, kt, P, aHn, aLn, kapn, integral_constant<int, 16>{});
-            }
-          }
-        } else if (cc == 0) {
+        if ((!LOSS || SHP == 2) && cp == 0 && cc == 0) dedupe_merge();
+        if (GS && gram_w && kt == 0 && (need_g || gs_step == 1)) gs_read();
+        // the next chunk's row DMAs right after the barrier, before a pass start's S7 / softmax / aux
+        // work (round 4: -0.9 %)
+        if (cc + 1 < nchunk) {
+          dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
+        } else {
+          item_offsets(ni, np, nH, nC, nLv);
+          dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
+        }
+        if (cc == 0) {
           did_s7 = (WITH_CAND && pend_off >= 0) || d_pending;
-          if (!S7LATE) {
-            if (WITH_CAND && pend_off >= 0) s7();
-            pend_off = -1;
-          }
-          if (R3 && WITH_CAND && wave == 4) {   // this pass's candidate units -> LDS (read by its S7, a pass later)
-            const int lane = threadIdx.x & 63;
-            const int id = l1_cand<R3>(smem, ci & 3)[min(64 * cp + min(lane, max(cntp, 1) - 1), kMaxCand - 1)];
-            dma_b32(p.unit_t + min(max(id, 0), p.n_news - 1), sbase + Cv::kOffUc + (pass_ctr & 1) * 256);
-          }
+          if (WITH_CAND && pend_off >= 0) s7();
+          pend_off = -1;
           if (LOSS && pend_d >= 0) form_d(pend_d);
           pend_d = -1;
           d_pending = false;
           if (cp == 0) {
             using std::integral_constant;
-            if (X2_SOFT_HALF && nkb == 1) softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 8>{});
+            // <= 32 history groups: the softmax over the first 32 only (the second block's A unused)
+            if (nkb == 1) softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 8>{});
             else softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 16>{});
-            if (LOSS && gram_w && dis_out) {
+            if (LOSS && !GS && gram_w && dis_out) {
               float kap1;                // interest tile 1 of the Gram: the Gram's cosines are per-k scale free
-              if (X2_SOFT_HALF && nkb == 1) softmax_inwave(ci, 1, 0, aH1, aL1, kap1, integral_constant<int, 8>{});
+              if (nkb == 1) softmax_inwave(ci, 1, 0, aH1, aL1, kap1, integral_constant<int, 8>{});
               else softmax_inwave(ci, 1, 0, aH1, aL1, kap1, integral_constant<int, 16>{});
             }
             dedupe_prep(ci + 2);       // L1 of ci + 2 landed; its logit rows are DMA'd by group next
@@ -1066,30 +1016,43 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
             issue_L0(ci + 4);
             issue_L1(ci + 3);
           }
+          if (GS && gs_step == 1) {
+            gs_step1();
+            gs_step = 2;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
         } else if (cc == 1 && cp == 0) {
           issue_L2(ci + 2);            // into the block impression ci's logits were read from
         }
-        if (S7LATE && cc == 1) {
-          if (WITH_CAND && pend_off >= 0) s7();
-          pend_off = -1;
+        if (GS && cc == 1 && gs_step == 2) {
+          gs_step2();
+          gs_step = 0;
         }
         X2_STAMP(2);
-        if (!X2_DMA_EARLY) issue_next();
         X2_STAMP(3);
         compute(ci, cc, mode, ntile);
       }
-      if (!R3 && WITH_CAND && wave >= 4) {
+      if (WITH_CAND && wave >= 4) {
         // this pass's S7 (after the next barrier) needs its candidates' row units: one per lane
         const int c = 16 * (wave & 3) + (int)(threadIdx.x & 15);
-        const int id = l1_cand<R3>(smem, ci & 3)[min(64 * cp + min(c, max(cntp, 1) - 1), kMaxCand - 1)];
+        const int id = l1_cand(smem, ci & 3)[min(64 * cp + min(c, max(cntp, 1) - 1), kMaxCand - 1)];
         uc_pend_r = p.unit_t[min(max(id, 0), p.n_news - 1)];
       }
-      pend_ub = pass_ctr & 1;
-      ++pass_ctr;
       if (nchunk == 1 && did_s7) raw_barrier();
-      if (LOSS && dis_out && cp == 0) {
+      if (GS && dis_out && cp == 0) {
+        // the four diagonal partials -> LDS [ch][kt][16] (read by step 1 after the next barrier)
+        if (gram_w) {
+          const int lane = threadIdx.x & 63;
+          const int j = lane & 15, g = lane >> 4;
+          float* gdg = reinterpret_cast<float*>(smem + Cv::kOffGram) + (2 * ch + kt) * 16;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * g + e == j) gdg[j] = gr[0][e];
+        }
+        gs_step = 1;
+        gs_b = imp_b(ci);
+      } else if (LOSS && dis_out && cp == 0) {
         // the Gram hand-off: wave 2 (columns 32..63 of each chunk) -> LDS -> wave 0 at the next chunk
         if (gram_w && ch == 1) {
           const int lane = threadIdx.x & 63;
@@ -1141,6 +1104,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   raw_barrier();
   if (WITH_CAND && pend_off >= 0) s7();
   if (LOSS && pend_d >= 0) form_d(pend_d);
+  if (GS && gs_step == 1) {
+    if (gram_w && kt == 0) gs_read();
+    gs_step1();
+    raw_barrier();
+    gs_step2();
+  }
 }
 
 // ================================================================================================
@@ -1163,14 +1132,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 // The masked slots holding the first masked slot's news id form one group (as news_score_x2).
 constexpr int kWRB = 128;                              // bytes per staged row piece (32 hi | 32 lo)
 constexpr int kWCTile = 16 * kWRB + 16;                // candidate tiles 16 B apart (see kCTile)
-// The carve by workgroup size. NW = 8: the wide form (K <= 64, L <= 128, one workgroup per CU).
-// NW = 4 (A/B, MINER_X2_W4): K <= 32, L <= 64, dense C <= 256, in 80 KB, two workgroups per CU —
-// each with its own barriers, so one workgroup's per-impression work runs beside the other's stream.
-template <int NW> struct XW {
-  static constexpr int kThr = 64 * NW;
-  static constexpr int kMaxL = NW == 8 ? MINER_NEWS_X2W_MAX_L : 64;
-  static constexpr int kMaxK = NW == 8 ? MINER_NEWS_X2W_MAX_K : 32;
-  static constexpr int kMaxC = NW == 8 ? kMaxCand : 256;
+// The carve of the wide form (K <= 64, L <= 128, one workgroup of 8 waves per CU)
+struct XW {
+  static constexpr int kThr = 512;
+  static constexpr int kMaxL = MINER_NEWS_X2W_MAX_L;
+  static constexpr int kMaxK = MINER_NEWS_X2W_MAX_K;
+  static constexpr int kMaxC = kMaxCand;
   static constexpr int kNKb = kMaxL / 32;                // history blocks of 32 groups
   static constexpr int kHalves = kMaxL / 64;             // 64-slot ballots of the dedupe
   static constexpr int kPart = kMaxL * kWRB;
@@ -1188,9 +1155,8 @@ template <int NW> struct XW {
   static constexpr int kOffDup = kOffPrep + 2 * kPrepB;  // per L1 slot: U
   static constexpr int kLds = kOffDup + 3 * kDupB;
 };
-static_assert(XW<8>::kMaxL == 128 && XW<8>::kMaxK == 64, "the wide carve is laid out for L <= 128, K <= 64");
-static_assert(XW<8>::kLds <= 160 * 1024, "news_score_x2w LDS");
-static_assert(XW<4>::kLds <= 80 * 1024, "news_score_x2w<4>: two workgroups per CU");
+static_assert(XW::kMaxL == 128 && XW::kMaxK == 64, "the wide carve is laid out for L <= 128, K <= 64");
+static_assert(XW::kLds <= 160 * 1024, "news_score_x2w LDS");
 
 // 16-byte chunk swizzle of a staged 128-byte row (8 chunks: hi 0..3, lo 4..7): slot = chunk ^
 // wswz(row). Over the 4 same-parity rows of a transposed read's 8-row group it takes the even
@@ -1199,9 +1165,10 @@ static_assert(XW<4>::kLds <= 80 * 1024, "news_score_x2w<4>: two workgroups per C
 // all 8 values: both reads are conflict-free (ds_read_b64 / _tr_b16 bank over 256 B per 32 lanes)
 __host__ __device__ inline int wswz(int row) { return (((row >> 1) & 3) << 1) | ((row >> 3) & 1); }
 
-template <int ST, bool RAGGED, int NW = 8>
-__global__ __launch_bounds__(64 * NW, 2) void news_score_x2w(X2Params p) {
-  using Cw = XW<NW>;
+template <int ST, bool RAGGED>
+__global__ __launch_bounds__(512, 2) void news_score_x2w(X2Params p) {
+  using Cw = XW;
+  constexpr int NW = 8;                                   // waves
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool WEIGHTED = ST == MINER_SCORE_WEIGHTED;
   constexpr bool WITH_CAND = ST != MINER_SCORE_NONE;
@@ -1259,10 +1226,10 @@ __global__ __launch_bounds__(64 * NW, 2) void news_score_x2w(X2Params p) {
         if (p.bias) dma_b32(p.bias + base, dst + 8 * Cw::kMaxL + 256 * hh);
       }
     }
-    if (WITH_CAND && (NW == 8 ? wave >= 4 : wave == 0)) {   // candidate ids, 64 per DMA
+    if (WITH_CAND && wave >= 4) {                       // candidate ids, 64 per DMA
       int off, cnt;
       cands(i, off, cnt);
-      for (int j = NW == 8 ? wave - 4 : 0; 64 * j < cnt; j += NW == 8 ? 4 : 1) {
+      for (int j = wave - 4; 64 * j < cnt; j += 4) {
         const int c = min(64 * j + lane, cnt - 1);
         dma_b32(p.cand_ids + off + c, dst + 12 * Cw::kMaxL + 256 * j);
       }
@@ -1677,12 +1644,8 @@ __global__ __launch_bounds__(64 * NW, 2) void news_score_x2w(X2Params p) {
           pend_off = -1;
           if (cp == 0) {
             using std::integral_constant;
-            if constexpr (NW == 8) {
-              if (nkb <= 2) softmax_w(ci, integral_constant<int, 16>{});
-              else softmax_w(ci, integral_constant<int, 32>{});
-            } else {
-              softmax_w(ci, integral_constant<int, 16>{});
-            }
+            if (nkb <= 2) softmax_w(ci, integral_constant<int, 16>{});
+            else softmax_w(ci, integral_constant<int, 32>{});
             dedupe_prep(ci + 1);
             issue_L0(ci + 3);
             issue_L1(ci + 2);
@@ -1751,93 +1714,62 @@ int x2_num_cus() {
 
 inline bool al16(const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; }
 
-template <int NW>
-int x2w_launch_nw(void* stream, const X2Params& prm) {
+int x2w_launch(void* stream, const X2Params& prm) {
   void (*kern)(X2Params) = nullptr;
   const bool rg = prm.cand_off != nullptr;
   switch (prm.score_type) {
-    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2w<MINER_SCORE_WEIGHTED, true, NW> : news_score_x2w<MINER_SCORE_WEIGHTED, false, NW>; break;
-    case MINER_SCORE_NONE: kern = news_score_x2w<MINER_SCORE_NONE, false, NW>; break;
-    default: kern = rg ? news_score_x2w<MINER_SCORE_MAX, true, NW> : news_score_x2w<MINER_SCORE_MAX, false, NW>; break;
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2w<MINER_SCORE_WEIGHTED, true> : news_score_x2w<MINER_SCORE_WEIGHTED, false>; break;
+    case MINER_SCORE_NONE: kern = news_score_x2w<MINER_SCORE_NONE, false>; break;
+    default: kern = rg ? news_score_x2w<MINER_SCORE_MAX, true> : news_score_x2w<MINER_SCORE_MAX, false>; break;
   }
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XW<NW>::kLds);
-  if (e != hipSuccess) return (int)e;
-  int grid = x2_num_cus() * (8 / NW);
-  if (grid > prm.B) grid = prm.B;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), XW<NW>::kLds, static_cast<hipStream_t>(stream), prm);
-  e = hipGetLastError();
-  return e == hipSuccess ? MINER_OK : (int)e;
-}
-int x2w_launch(void* stream, const X2Params& prm) { return x2w_launch_nw<8>(stream, prm); }
-
-// the two-workgroups-per-CU form (A/B: MINER_X2_W4=1): K <= 32, L <= 64, dense C <= 256, no eval loss
-#ifndef X2_W4
-#define X2_W4 0
-#endif
-bool x2w4_wanted(const X2Params& prm) {
-  const char* e = getenv("MINER_X2_W4");
-  return (e ? e[0] == '1' : X2_W4 != 0) && prm.K <= 32 && prm.L <= 64 && !prm.cand_off && prm.C <= 256 && !prm.dis_out;
-}
-
-#ifndef X2_FORCE_WIDE
-#define X2_FORCE_WIDE 0   // A/B only: every shape through news_score_x2w
-#endif
-int x2_launch(void* stream, const X2Params& prm) {
-  if (prm.L > kMaxL || prm.K > kMaxK || (X2_FORCE_WIDE && !prm.dis_out)) return x2w_launch(stream, prm);
-  if (x2w4_wanted(prm)) return x2w_launch_nw<4>(stream, prm);
-  void (*kern)(X2Params) = nullptr;
-  int lds = kX2Lds;
-  const bool rg = prm.cand_off != nullptr;
-  if (prm.dis_out) {                   // eval with the eval loss (config/eval_miner.txt: metrics + loss)
-#define X2_PICKL(NCHV)                                                                                       \
-    switch (prm.score_type) {                                                                                \
-      case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, NCHV, 0, true> : news_score_x2<MINER_SCORE_WEIGHTED, false, NCHV, 0, true>; break; \
-      case MINER_SCORE_NONE: kern = news_score_x2<MINER_SCORE_NONE, false, NCHV, 0, true>; break;             \
-      default: kern = rg ? news_score_x2<MINER_SCORE_MAX, true, NCHV, 0, true> : news_score_x2<MINER_SCORE_MAX, false, NCHV, 0, true>; break; \
-    }
-    // the MIND shape with no bias and no mui output (the reference's default eval) compile-time, as
-    // the plain-scoring form below
-    const bool plainl = prm.L == 50 && prm.K == 32 && !prm.bias && !prm.mui_out &&
-                        prm.score_type == MINER_SCORE_WEIGHTED && !getenv("MINER_NEWS_SHP_RT");
-    if (prm.d == 768) {
-      if (plainl) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 12, 2, true> : news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2, true>;
-      else { X2_PICKL(12) }
-    } else if (prm.d == 256 && plainl) {   // config 2 (MIND-small)
-      kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 4, 2, true> : news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2, true>;
-    } else {
-      X2_PICKL(0)
-    }
-#undef X2_PICKL
-  } else {
-#define X2_PICK(NCHV)                                                                                        \
-  switch (prm.score_type) {                                                                                  \
-    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, NCHV, 0> : news_score_x2<MINER_SCORE_WEIGHTED, false, NCHV, 0>; break; \
-    case MINER_SCORE_NONE: kern = news_score_x2<MINER_SCORE_NONE, false, NCHV, 0>; break;                     \
-    default: kern = rg ? news_score_x2<MINER_SCORE_MAX, true, NCHV, 0> : news_score_x2<MINER_SCORE_MAX, false, NCHV, 0>; break; \
-  }
-  const bool plain = prm.L == 50 && prm.K == 32 && !prm.bias && !prm.mui_out && prm.score_type == MINER_SCORE_WEIGHTED &&
-                     !getenv("MINER_NEWS_SHP_RT");
-  // the 3-slot ring (two chunks in flight): the MIND shape with dense candidates, at most 48 of them
-  const char* r3e = getenv("MINER_X2_RING3");
-  const bool ring3 = plain && !rg && prm.C <= 48 && (r3e ? r3e[0] == '1' : X2_RING3 != 0);
-  if (prm.d == 768) {                  // config 3 (MIND-large): the chunk count compile-time
-    if (ring3) { kern = news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2, false, true>; lds = X2C<true>::kLds; }
-    else if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 12, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 12, 2>;
-    else { X2_PICK(12) }
-  } else if (prm.d == 256) {           // config 2 (MIND-small)
-    if (ring3) { kern = news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2, false, true>; lds = X2C<true>::kLds; }
-    else if (plain) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, 4, 2> : news_score_x2<MINER_SCORE_WEIGHTED, false, 4, 2>;
-    else { X2_PICK(4) }
-  } else {
-    X2_PICK(0)
-  }
-  }
-#undef X2_PICK
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XW::kLds);
   if (e != hipSuccess) return (int)e;
   int grid = x2_num_cus();
   if (grid > prm.B) grid = prm.B;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, static_cast<hipStream_t>(stream), prm);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(XW::kThr), XW::kLds, static_cast<hipStream_t>(stream), prm);
+  e = hipGetLastError();
+  return e == hipSuccess ? MINER_OK : (int)e;
+}
+
+// The kernel for a launch: the MIND shape (history 50, K = 32, 'weighted', no category bias, no mui
+// output; the bench and the reference's eval) with its chunk count and shape compile-time, every
+// other shape the run-time form
+int x2_launch(void* stream, const X2Params& prm) {
+  if (prm.L > kMaxL || prm.K > kMaxK) return x2w_launch(stream, prm);
+  void (*kern)(X2Params) = nullptr;
+  const bool rg = prm.cand_off != nullptr;
+  const bool mind = prm.L == 50 && prm.K == 32 && !prm.bias && !prm.mui_out && prm.score_type == MINER_SCORE_WEIGHTED;
+#define X2_PICK(NCHV, LOSSV)                                                                                 \
+  switch (prm.score_type) {                                                                                  \
+    case MINER_SCORE_WEIGHTED: kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, NCHV, 0, LOSSV> : news_score_x2<MINER_SCORE_WEIGHTED, false, NCHV, 0, LOSSV>; break; \
+    case MINER_SCORE_NONE: kern = news_score_x2<MINER_SCORE_NONE, false, NCHV, 0, LOSSV>; break;              \
+    default: kern = rg ? news_score_x2<MINER_SCORE_MAX, true, NCHV, 0, LOSSV> : news_score_x2<MINER_SCORE_MAX, false, NCHV, 0, LOSSV>; break; \
+  }
+#define X2_MIND(NCHV, LOSSV) kern = rg ? news_score_x2<MINER_SCORE_WEIGHTED, true, NCHV, 2, LOSSV> : news_score_x2<MINER_SCORE_WEIGHTED, false, NCHV, 2, LOSSV>
+  if (prm.dis_out) {                   // eval with the eval loss (config/eval_miner.txt: metrics + loss)
+    if (prm.d == 768) {
+      if (mind) { X2_MIND(12, true); } else { X2_PICK(12, true) }
+    } else if (prm.d == 256 && mind) {   // config 2 (MIND-small)
+      X2_MIND(4, true);
+    } else {
+      X2_PICK(0, true)
+    }
+  } else {
+    if (prm.d == 768) {                // config 3 (MIND-large)
+      if (mind) { X2_MIND(12, false); } else { X2_PICK(12, false) }
+    } else if (prm.d == 256) {         // config 2 (MIND-small)
+      if (mind) { X2_MIND(4, false); } else { X2_PICK(4, false) }
+    } else {
+      X2_PICK(0, false)
+    }
+  }
+#undef X2_PICK
+#undef X2_MIND
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kX2Lds);
+  if (e != hipSuccess) return (int)e;
+  int grid = x2_num_cus();
+  if (grid > prm.B) grid = prm.B;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), kX2Lds, static_cast<hipStream_t>(stream), prm);
   e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;
 }
@@ -1879,7 +1811,7 @@ int miner_score_news_x2(void* stream, int score_type, const void* table2, const 
   if (score_type < MINER_SCORE_WEIGHTED || score_type > MINER_SCORE_NONE) return MINER_EINVAL;
   if (!table2 || !table_unit || !news_logits || !his_ids || !his_mask || n_news <= 0 || B < 0) return MINER_EINVAL;
   if (L <= 0 || d <= 0 || K <= 0) return MINER_EINVAL;
-  if (L > XW<8>::kMaxL || K > XW<8>::kMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
+  if (L > XW::kMaxL || K > XW::kMaxK || (K & 3) || d % 64 || d > 1024) return MINER_ESHAPE;
   if ((L > kMaxL || K > kMaxK) && disagree_out) return MINER_ESHAPE;   // the wide kernel writes mui instead
   if ((uint64_t)n_news * (uint64_t)d * 4u > 0xffffffffull) return MINER_ESHAPE;   // 32-bit row offsets
   if (score_type == MINER_SCORE_WEIGHTED && (!proj2 || !proj_unit)) return MINER_EINVAL;

@@ -287,7 +287,9 @@ def score(nt: NewsTable, his_ids: Tensor, his_mask: Tensor, cand_ids: Optional[T
                                                 _ptr(his_bias), _ptr(cid), _ptr(offs), B, L, C, d, K, _ptr(scores),
                                                 _ptr(mui), _ptr(dis))
         else:
-            rc = _lib.lib().miner_score_news(_stream(dev), dt, st, _ptr(nt.table), _ptr(nt.logits), _ptr(nt.proj),
+            # MINER_NEWS_F32X6=1 (read per call, a Python-side switch): news_score32's bf16x6 form
+            kdt = _lib.DTYPE_F32_X6 if dt == _lib.DTYPE_F32 and os.environ.get("MINER_NEWS_F32X6") else dt
+            rc = _lib.lib().miner_score_news(_stream(dev), kdt, st, _ptr(nt.table), _ptr(nt.logits), _ptr(nt.proj),
                                              nt.n_news, _ptr(hid), _ptr(mask), _ptr(his_bias), _ptr(cid), _ptr(offs),
                                              B, L, C, d, K, _ptr(scores), _ptr(mui))
     _lib.check(rc, "miner_score_news_x2" if use_x2 else "miner_score_news")

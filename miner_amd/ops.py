@@ -10,6 +10,7 @@ raw ``(w_poly, context_codes, w_target)`` tensors and packs them on the fly.
 from __future__ import annotations
 
 import dataclasses
+import os
 
 import torch
 
@@ -37,6 +38,15 @@ def _contig(t, dtype=None):
     if dtype is not None and t.dtype != dtype:
         t = t.to(dtype)
     return t.contiguous()
+
+
+def _kernel_dtype(dt: int) -> int:
+    """The dtype code a dense-row launch passes: fp32 runs its S1 / S5 contractions as bf16x6 by
+    default; MINER_DENSE_FP32=mfma32 (read per call, a Python-side switch) asks the library for the
+    exact fp32-MFMA form (MINER_DTYPE_F32_MFMA)."""
+    if dt == _lib.DTYPE_F32 and os.environ.get("MINER_DENSE_FP32") == "mfma32":
+        return _lib.DTYPE_F32_MFMA
+    return dt
 
 
 def _dtype_code(dtype: torch.dtype) -> int:
@@ -257,7 +267,7 @@ def score(history: torch.Tensor, his_mask: torch.Tensor, candidates: torch.Tenso
                            scores.numel(), return_user)
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32) if return_user else None
     with torch.cuda.device(history.device):
-        rc = _lib.lib().miner_score(_stream(history.device), dt, st, _ptr(history), _ptr(mask), _ptr(his_bias),
+        rc = _lib.lib().miner_score(_stream(history.device), _kernel_dtype(dt), st, _ptr(history), _ptr(mask), _ptr(his_bias),
                                     _ptr(candidates), _ptr(offs), _ptr(pw.buf), B, L, C, d, Dc, K,
                                     _ptr(scores), _ptr(mui))
     _lib.check(rc, "miner_score")
@@ -330,7 +340,7 @@ def score_gather(news_table: torch.Tensor, his_ids: torch.Tensor, his_mask: torc
         return _score_wide(pw, st, table, hid, mask, his_bias, table, cid, offs, B, C, scores.numel(), return_user)
     mui = torch.empty((B, K, d), device=table.device, dtype=torch.float32) if return_user else None
     with torch.cuda.device(table.device):
-        rc = _lib.lib().miner_score_gather(_stream(table.device), dt, st, _ptr(table), n_news, _ptr(hid), _ptr(mask),
+        rc = _lib.lib().miner_score_gather(_stream(table.device), _kernel_dtype(dt), st, _ptr(table), n_news, _ptr(hid), _ptr(mask),
                                            _ptr(his_bias), _ptr(cid), _ptr(offs), _ptr(pw.buf), B, L, C, d, Dc, K,
                                            _ptr(scores), _ptr(mui))
     _lib.check(rc, "miner_score_gather")
@@ -359,7 +369,7 @@ def poly_attention(history: torch.Tensor, his_mask: torch.Tensor, w_poly, contex
         return res[0] if tdt == torch.float32 else res[2]
     mui = torch.empty((B, K, d), device=history.device, dtype=torch.float32)
     with torch.cuda.device(history.device):
-        rc = _lib.lib().miner_score(_stream(history.device), dt, _lib.SCORE_NONE, _ptr(history), _ptr(mask),
+        rc = _lib.lib().miner_score(_stream(history.device), _kernel_dtype(dt), _lib.SCORE_NONE, _ptr(history), _ptr(mask),
                                     _ptr(his_bias), None, None, _ptr(pw.buf), B, L, 0, d, Dc, K, None, _ptr(mui))
     _lib.check(rc, "miner_score(PolyAttention)")
     return mui
@@ -427,7 +437,7 @@ def target_aware(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, w_
         _lib.check(rc, "miner_score_wide")
         return out
     with torch.cuda.device(query.device):
-        rc = _lib.lib().miner_target_aware(_stream(query.device), dt, _ptr(query), _ptr(key), _ptr(value), _ptr(offs),
+        rc = _lib.lib().miner_target_aware(_stream(query.device), _kernel_dtype(dt), _ptr(query), _ptr(key), _ptr(value), _ptr(offs),
                                            _ptr(pw.buf), pw.Dc, B, C, d, K, _ptr(out))
     _lib.check(rc, "miner_target_aware")
     return out

@@ -188,3 +188,45 @@ def test_config5_bench_step_fp16():
     sub = torch.tensor(users, device=DEV)
     s2, i2 = corpus.rank_topk(mui[sub], proj[sub], table, topk)
     assert torch.equal(s2, top_s[sub]) and torch.equal(i2, top_i[sub])
+
+
+def test_config5_per_gpu_share_fp16():
+    """BASELINE config 5 at one GPU's share of its 1M users (8 GPUs: 125,000 users each) against the
+    200,000-news fp16 table, history 200, K = 64, top-100, in one host loop (corpus.rank_corpus,
+    16,384 users per encode + rank pair). Sampled users — batch boundaries included — against the
+    oracle's full 200k scores from their own 16-bit user vectors (RANK16_TOL as above), no news
+    outside a list above its last entry; and the first 20,000 users ranked in batches of 7,000 give
+    the same lists bit for bit (batch independence)."""
+    from miner_amd import corpus
+    from oracle import corpus_oracle as co
+    U, L, K, N, d, topk = 125_000, 200, 64, 200_000, 768, 100
+    rtol = rms_floor = 2e-4
+    g = torch.Generator(device=DEV).manual_seed(55)
+    table = (torch.randn((N, d), generator=g, device=DEV) / d ** 0.5).to(torch.float16)
+    W1, Q, W2 = synthetic.init_weights(55, d, 200, K, device=DEV)
+    pk = corpus.pack_encoder(W1, Q, W2, dtype=torch.float16)
+    hid = torch.randint(0, N, (U, L), generator=g, device=DEV, dtype=torch.int32)
+    lens = torch.randint(1, L + 1, (U,), generator=g, device=DEV)
+    mask = torch.arange(L, device=DEV)[None, :] >= (L - lens)[:, None]
+    top_s, top_i = corpus.rank_corpus(table, hid, mask, pk, topk)
+    torch.cuda.synchronize()
+    assert torch.isfinite(top_s).all() and bool((top_i >= 0).all())
+    users = [0, 16383, 16384, 77777, 124999]
+    sub = torch.tensor(users, device=DEV)
+    mui, proj = corpus.encode_users(table, mask[sub], pk, his_ids=hid[sub])
+    T = table.float().cpu()
+    with torch.no_grad():
+        full = co.corpus_scores(mui.float().cpu(), proj.float().cpu(), T)      # [5, N] fp32
+    rms = float(full.pow(2).mean().sqrt())
+    for r, u in enumerate(users):
+        got_i = top_i[u].cpu().long()
+        assert len(set(got_i.tolist())) == topk
+        true = full[r, got_i].double()
+        err = (top_s[u].cpu().double() - true).abs()
+        assert bool((err <= rtol * true.abs() + rms_floor * rms).all()), (u, float(err.max()))
+        kth = float(true.min())
+        outside = torch.ones(N, dtype=torch.bool)
+        outside[got_i] = False
+        assert float(full[r, outside].max()) <= kth + rms_floor * rms + rtol * abs(kth), u
+    s2, i2 = corpus.rank_corpus(table, hid[:20000], mask[:20000], pk, topk, batch=7000)
+    assert torch.equal(s2, top_s[:20000]) and torch.equal(i2, top_i[:20000])

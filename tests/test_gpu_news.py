@@ -374,45 +374,32 @@ def test_masked_slot_groups(dtype, monkeypatch):
     _ok(s_plain, ref_plain, dtype, "plain scores")
 
 
-@pytest.mark.parametrize("d,C", [(768, 40), (768, 48), (256, 40), (768, 33)])
-def test_x2_ring3_equals_ring2(d, C, monkeypatch):
-    """The 3-slot ring (two chunks in flight; the MIND shape L = 50, K = 32, plain scoring, dense
-    candidates, C <= 48) gives the 2-slot kernel's scores bit for bit, and the oracle's at the fp32
-    bar; padded and full histories, several impressions per workgroup."""
-    monkeypatch.setenv("MINER_NEWS_FP32", "x2")
-    B = 1200
-    table, hid, mask, cid, offs, W1, Q, W2 = _setup(40 + C, B, 50, d, 4000, torch.float32, C=C)
-    mask[:100] = True                                    # full histories: 50 groups, both blocks
-    nt = news.precompute(table, W1, Q, W2)
-    monkeypatch.setenv("MINER_X2_RING3", "1")
-    s3 = news.score(nt, hid, mask, cid)
-    monkeypatch.setenv("MINER_X2_RING3", "0")
-    s2 = news.score(nt, hid, mask, cid)
+def test_spread_gram_nonfinite_row_isolated():
+    """The spread Gram (MIND-shape LOSS kernel) hands each chunk's interest-tile-1 operand to the
+    tile-0 wave through ring rows the history product reads times an attention weight of 0: an
+    impression whose history holds an infinite table element must not leak NaN into the impressions
+    that the same workgroup scores after it (4 per workgroup here). Its own D is not finite, as the
+    reference's cosines of an infinite mui (utils.py:9-29); every other impression's D and scores
+    match the oracle at the fp32 bar."""
+    from miner_amd import evaluation
+    B, L, d, n_news = 4 * 256, 50, 768, 3000
+    table, hid, mask, cid, offs, W1, Q, W2 = _setup(717, B, L, d, n_news, torch.float32)
+    bad_row, bad_imp = n_news - 1, 5
+    hid[hid == bad_row] = 1
+    cid[cid == bad_row] = 1
+    hid[bad_imp, -1] = bad_row
+    mask[bad_imp, -1] = True
+    table[bad_row, 7] = float("inf")
+    nt = news.precompute(table, W1, Q, W2, x2=True)
+    s, dis = news.score(nt, hid, mask, cid, x2=True, disagreement=True)
     torch.cuda.synchronize()
-    assert torch.equal(s3, s2), float((s3 - s2).abs().max())
-    _, ref = _oracle(table, hid, mask, cid, None, W1, Q, W2)
-    _ok(s3, ref, torch.float32, "ring-3 scores")
-
-
-@pytest.mark.parametrize("d,C,bias,mui", [(768, 40, False, False), (256, 40, True, True), (64, 5, False, True),
-                                          (768, 150, True, False)])
-def test_x2_two_workgroups_per_cu(d, C, bias, mui, monkeypatch):
-    """The two-workgroups-per-CU form of the pair-plane kernel (news_score_x2w<4>, MINER_X2_W4=1:
-    4 waves and 80 KB per workgroup, dense candidates <= 256) against the oracle at the fp32 bar:
-    scores and mui, with and without category bias, three candidate passes."""
-    monkeypatch.setenv("MINER_NEWS_FP32", "x2")
-    monkeypatch.setenv("MINER_X2_W4", "1")
-    B = 700
-    table, hid, mask, cid, offs, W1, Q, W2 = _setup(70 + d + C, B, 50, d, 3000, torch.float32, C=C)
-    hb = (torch.rand(hid.shape, device=DEV) - 0.5) if bias else None
-    nt = news.precompute(table, W1, Q, W2)
-    out = news.score(nt, hid, mask, cid, his_bias=hb, return_user=mui)
-    torch.cuda.synchronize()
-    s, m = out if mui else (out, None)
-    ref_mui, ref = _oracle(table, hid, mask, cid, None, W1, Q, W2, bias=hb)
-    _ok(s, ref, torch.float32, "scores")
-    if mui:
-        _ok(m, ref_mui, torch.float32, "mui")
+    assert not torch.isfinite(dis[bad_imp]).item()
+    keep = torch.ones(B, dtype=torch.bool, device=DEV)
+    keep[bad_imp] = False
+    ref_mui, ref_s = _oracle(table, hid[keep], mask[keep], cid[keep], None, W1, Q, W2)
+    _ok(s[keep], ref_s, torch.float32, "scores of the other impressions")
+    ref = evaluation.disagreement(ref_mui.double()).float()
+    _ok(dis[keep], ref, torch.float32, "disagreement of the other impressions")
 
 
 def test_x2_nan_logit_propagates(monkeypatch):
@@ -498,24 +485,23 @@ def test_bad_inputs_raise():
     (90, 64, 128, 33, 16, None),       # L = 64, K = 16 (interest tile 1 empty)
     (40, 37, 320, 150, 12, None),      # three candidate passes
     (211, 50, 768, None, 32, (0, 150)),  # ragged 0..150 candidates (compile-time LOSS kernel unless shp_rt)
+    (130, 50, 768, 150, 32, None),     # MIND shape, three candidate passes per impression (spread Gram)
 ])
-def test_fused_disagreement(B, L, d, C, K, ragged, shp_rt, monkeypatch):
+def test_fused_disagreement(B, L, d, C, K, ragged, shp_rt):
     """The eval loss's disagreement term formed inside the fp32 scoring kernel (the Gram matrix of
     mui, no mui written) equals the reference formula on the reference's own mui (float64), and the
-    scores of the loss variant match the plain kernel's at the fp32 bar. With shp_rt unset the MIND
-    shape (L = 50, K = 32, no bias, no mui output) runs the compile-time LOSS kernels
-    (news_score_x2<WEIGHTED, *, 12 | 4, 2, true>) that eval_loop's fused-loss path launches by
-    default; their D and scores must also match the run-time-shape form's."""
-    if shp_rt:
-        monkeypatch.setenv("MINER_NEWS_SHP_RT", "1")
-    else:
-        monkeypatch.delenv("MINER_NEWS_SHP_RT", raising=False)
+    scores of the loss variant match the plain kernel's at the fp32 bar. The MIND shape (L = 50,
+    K = 32, no bias, no mui output) runs the compile-time LOSS kernels (news_score_x2<WEIGHTED, *,
+    12 | 4, 2, true>, the Gram spread over the four mui waves) that eval_loop's fused-loss path
+    launches by default; shp_rt adds an all-zero category bias, which adds exactly 0 to every logit
+    and selects the run-time-shape form (the Gram on two waves): both forms' D and scores must agree."""
     from miner_amd import evaluation
     table, hid, mask, cid, offs, W1, Q, W2 = _setup(B + d + K, B, L, d, 2000, torch.float32, C=C or 40, K=K,
                                                     ragged=ragged)
+    zb = torch.zeros(hid.shape, device=DEV) if shp_rt else None
     nt = news.precompute(table, W1, Q, W2, x2=True)
     s_plain = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True)
-    s, dis = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True, disagreement=True)
+    s, dis = news.score(nt, hid, mask, cid, cand_offsets=offs, his_bias=zb, x2=True, disagreement=True)
     torch.cuda.synchronize()
     # same arithmetic; hipcc may contract a multiply-add differently in the two instantiations
     _ok(s, s_plain, torch.float32, "loss-variant scores vs the plain kernel")
@@ -525,10 +511,9 @@ def test_fused_disagreement(B, L, d, C, K, ragged, shp_rt, monkeypatch):
     _ok(dis, ref, torch.float32, "disagreement")
     if not shp_rt:
         # the compile-time-shape kernels against the run-time form on the same inputs
-        monkeypatch.setenv("MINER_NEWS_SHP_RT", "1")
-        s_rt, dis_rt = news.score(nt, hid, mask, cid, cand_offsets=offs, x2=True, disagreement=True)
+        s_rt, dis_rt = news.score(nt, hid, mask, cid, cand_offsets=offs, his_bias=torch.zeros(hid.shape, device=DEV),
+                                  x2=True, disagreement=True)
         torch.cuda.synchronize()
-        monkeypatch.delenv("MINER_NEWS_SHP_RT")
         _ok(s, s_rt, torch.float32, "compile-time-shape LOSS scores vs the run-time form")
         _ok(dis, dis_rt, torch.float32, "compile-time-shape disagreement vs the run-time form")
     # mui-only launch with the loss epilogue (score type 'none')

@@ -3,7 +3,8 @@ extra flags, each built alone): the same precomputed tables and impressions (con
 bench's synthetic ids), median ms per launch and max |score difference| against the first build.
 
     python tools/x2_ab.py --build NAME [REV|-] [FLAGS...]   # CPU: tools/bisect/libx2_NAME.so
-    python tools/x2_ab.py NAME1 NAME2 ... [--B N]          # GPU (X2AB_LOSS=1: with the disagreement)
+    python tools/x2_ab.py NAME1 NAME2 ... [--B N]          # GPU (X2AB_LOSS=1: with the disagreement;
+                                                          # NAME@loss: that entry alone with it)
 """
 import ctypes
 import os
@@ -50,14 +51,16 @@ def run(names, B=1_000_000, reps=5, d=768, n_news=104000):
     st = torch.cuda.current_stream().cuda_stream
     libs = {}
     for n in names:
-        h = ctypes.CDLL(os.path.join(OUT, f"libx2_{n}.so"))
+        h = ctypes.CDLL(os.path.join(OUT, f"libx2_{n.split('@')[0]}.so"))
         h.miner_score_news_x2.argtypes = [P, I, P, P, P, P, P, I, P, P, P, P, P, I, I, I, I, I, P, P, P]
         libs[n] = h
     out = {n: torch.empty(B * C, device=dev) for n in names}
-    loss = os.environ.get("X2AB_LOSS") == "1"          # with the eval loss's disagreement output
-    dis = {n: torch.empty(B, device=dev) for n in names} if loss else None
+    loss_all = os.environ.get("X2AB_LOSS") == "1"      # with the eval loss's disagreement output
+    lossn = {n: loss_all or n.endswith("@loss") for n in names}
+    dis = {n: torch.empty(B, device=dev) for n in names}
 
     def launch(n):
+        loss = lossn[n]
         px = nt.x2
         rc = libs[n].miner_score_news_x2(st, 0, px.table2.data_ptr(), px.table_unit.data_ptr(), nt.logits.data_ptr(),
                                          px.proj2.data_ptr(), px.proj_unit.data_ptr(), n_news, beh.his_ids.data_ptr(),
@@ -79,7 +82,7 @@ def run(names, B=1_000_000, reps=5, d=768, n_news=104000):
             times[n].append(a.elapsed_time(b))
     for n in names:
         diff = float((out[n] - out[names[0]]).abs().max())
-        if loss:
+        if lossn[n] and lossn[names[0]]:
             diff = max(diff, float((dis[n] - dis[names[0]]).abs().max()))
         t = statistics.median(times[n])
         print(f"{n}: {t:.3f} ms per {B} impressions ({B * C / t / 1e3:.1f} M pairs/s), all "
