@@ -65,6 +65,7 @@ namespace {
 #ifndef X2_ABL
 #define X2_ABL 0
 #endif
+
 // (eval-loss form, GS: 64 no diagonal Gram tile, 128 no operand exchange / off-diagonal tile, 256 no
 // per-chunk Gram work, 512 no per-impression D step)
 constexpr int kNB = 2;                                // row-DMA blocks per wave per part
@@ -845,6 +846,19 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // the products of one chunk in slot t & 1 (after the next chunk's row DMAs, issued first so that
   // they land before the next barrier); mode: 1 history product, 2 candidate product, 4 mui out,
   // 8 Gram; NT candidate tiles compile-time (0: no candidate product)
+  // the next chunk's row DMAs, issued by every wave right after the barrier. (Round 6 A/B,
+  // tools/x2_ab.py, 1M impressions: the mui waves — which set the chunk length — issuing theirs
+  // after their history product instead +3.1 %; the mui waves at priority 2 while they issue
+  // +2.2 %; profiles/r06_x2_dma_ab.txt)
+  int dn_cc = 0, dn_ni = 0, dn_np = 0;
+  auto issue_dmas = [&]() {
+    if (dn_cc + 1 < nchunk) {
+      dma_chunk(cH, cC, cLv, dn_cc + 1, (t + 1) & 1);
+    } else {
+      item_offsets(dn_ni, dn_np, nH, nC, nLv);
+      dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
+    }
+  };
   auto compute_t = [&](int ci, int cc, int mode, auto nt_c) {
     constexpr int NT = decltype(nt_c)::value;
     FRESH_LANE_IDS();
@@ -985,12 +999,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         if (GS && gram_w && kt == 0 && (need_g || gs_step == 1)) gs_read();
         // the next chunk's row DMAs right after the barrier, before a pass start's S7 / softmax / aux
         // work (round 4: -0.9 %)
-        if (cc + 1 < nchunk) {
-          dma_chunk(cH, cC, cLv, cc + 1, (t + 1) & 1);
-        } else {
-          item_offsets(ni, np, nH, nC, nLv);
-          dma_chunk(nH, nC, nLv, 0, (t + 1) & 1);
-        }
+        dn_cc = cc; dn_ni = ni; dn_np = np;
+        issue_dmas();
+        X2_STAMP(3);
         if (cc == 0) {
           did_s7 = (WITH_CAND && pend_off >= 0) || d_pending;
           if (WITH_CAND && pend_off >= 0) s7();
@@ -1030,7 +1041,6 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           gs_step = 0;
         }
         X2_STAMP(2);
-        X2_STAMP(3);
         compute(ci, cc, mode, ntile);
       }
       if (WITH_CAND && wave >= 4) {

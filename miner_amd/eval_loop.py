@@ -107,8 +107,9 @@ def evaluate(packed: "ops.PackedWeights", table: torch.Tensor, beh: "synthetic.B
     total_samples = int(offs[-1]) if total_samples is None else total_samples
     L, d = beh.his_ids.shape[1], table.shape[1]
     max_c = 1 if category is not None else _max_candidates(offs, beh.n)
-    news_ok = news.path_supported(table.dtype, L, d, packed.Dc, packed.K)
-    news_wide = news.wide_supported(table.dtype, L, d, packed.Dc, packed.K)   # K > 32 or L > 64 (news_score_x2w)
+    news_ok = news.path_supported(table.dtype, L, d, packed.Dc, packed.K, n_news=table.shape[0])
+    news_wide = news.wide_supported(table.dtype, L, d, packed.Dc, packed.K,
+                                    n_news=table.shape[0])   # K > 32 or L > 64 (news_score_x2w)
     if scorer == "news":
         if not news_ok:
             raise ValueError(f"scorer='news': the news path does not support L={L} d={d} K={packed.K}")

@@ -72,18 +72,21 @@ def supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int) -> bool:
     return _lib.lib().miner_news_supported(_dtype_code(dtype), L, d, Dc, K) == 0
 
 
-def wide_supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int) -> bool:
+def wide_supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int, n_news: Optional[int] = None) -> bool:
     """Shapes past the news kernels' K <= 32 / L <= 64 that the fp32 pair-plane kernel scores in its
     wide form (news_score_x2w: K <= 64, L <= 128, K % 4 == 0): fp32 tables with pair planes only
-    (not under MINER_NEWS_FP32=mfma32), no in-kernel disagreement (the eval loss uses mui)."""
+    (not under MINER_NEWS_FP32=mfma32), no in-kernel disagreement (the eval loss uses mui). With
+    ``n_news``, the table must also fit the pair planes' 32-bit row offsets (x2_fits): precompute
+    builds no pair planes past them, and the wide form has no other input."""
     return (dtype == torch.float32 and x2_enabled() and not supported(dtype, L, d, Dc, K)
             and 0 < L <= X2W_MAX_L and 0 < K <= X2W_MAX_K and K % 4 == 0
-            and supported(dtype, 1, d, Dc, min(K, FUSED_MAX_K)))
+            and supported(dtype, 1, d, Dc, min(K, FUSED_MAX_K))
+            and (n_news is None or x2_fits(n_news, d)))
 
 
-def path_supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int) -> bool:
-    """The news-id path takes (dtype, L, d, Dc, K): the news kernels or the wide pair-plane form."""
-    return supported(dtype, L, d, Dc, K) or wide_supported(dtype, L, d, Dc, K)
+def path_supported(dtype: torch.dtype, L: int, d: int, Dc: int, K: int, n_news: Optional[int] = None) -> bool:
+    """The news-id path takes (dtype, L, d, Dc, K[, n_news]): the news kernels or the wide pair-plane form."""
+    return supported(dtype, L, d, Dc, K) or wide_supported(dtype, L, d, Dc, K, n_news)
 
 
 def _check_shape(dt: int, L: int, d: int, Dc: int, K: int) -> None:

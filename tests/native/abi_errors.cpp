@@ -45,7 +45,7 @@ int main() {
     if (!s || strlen(s) > 200) { fprintf(stderr, "FAIL miner_strerror(%d)\n", c); ++g_fail; }
   }
   if (miner_abi_version() != MINER_ABI_VERSION) { fprintf(stderr, "FAIL abi version\n"); ++g_fail; }
-  const int dts[] = {-1, 0, 1, 2, 3, 1 << 30};
+  const int dts[] = {-1, 0, 1, 2, 3, 4, 5, 1 << 30};
   const int dims[] = {-2147483647 - 1, -1, 0, 1, 31, 32, 64, 768, 1 << 20, 2147483647};
   for (int dt : dts)
     for (int d : dims) {
@@ -61,9 +61,12 @@ int main() {
       (void)miner_fastformer_packed_bytes(dt);
       (void)miner_fastformer_lds_bytes(dt);
       (void)miner_rank_topk_workspace_bytes(d, d);
+      (void)miner_rank_topk_split_recommended(d);
       (void)miner_auc_workspace_bytes((int64_t)d * 4096);
     }
   EXPECT(miner_supported(7, 50, 768, 200, 32), MINER_EINVAL);
+  EXPECT(miner_supported(MINER_DTYPE_F32_X6, 50, 768, 200, 32), MINER_EINVAL);   // a news-path form only
+  EXPECT(miner_news_precompute(st, MINER_DTYPE_F32_X6, buf, 100, buf, 768, 200, 32, fo, buf), MINER_EINVAL);
   EXPECT(miner_supported(0, 50, 100, 200, 32), 0);          // d % 32
   EXPECT(miner_supported(0, 200, 768, 200, 32), 0);         // L > 64
 

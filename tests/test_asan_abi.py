@@ -4,7 +4,10 @@ with tests/native/abi_errors.cpp (miner_amd/build.py::build_asan_driver), a CPU 
 every entry point of include/*.h with null / misaligned pointers, bad enums, negative and oversized
 shapes, and sweeps the host-only queries (miner_strerror, *_supported, *_bytes) over extreme values.
 Each call must return its MINER_E* code before any device work, and ASan must report nothing. No
-GPU is needed (no call reaches HIP); GPU-side sanitizers are not available on this pool.
+GPU is needed: no call launches or touches device memory. Two host queries ask the HIP runtime for
+the device's CU count (miner_rank_topk_workspace_bytes / miner_rank_topk_split_recommended, through
+the cached num_cus(), which answers 256 when no device is present); GPU-side sanitizers are not
+available on this pool.
 
 The first run compiles the library again (~2-3 min on 8 CPUs); later runs reuse build/asan/."""
 import os
