@@ -311,7 +311,8 @@ def load_pmc(path, workload, B, family):
         PMC_STATUS[key] = f"unreadable: {type(e).__name__}"
         return None
     want = source_sha16(KERNEL_SOURCES[family])
-    sym = "news_score_x2" if family == "news_x2" else "news_score" if family == "news" else "miner_fused"
+    sym = {"news_x2": "news_score_x2", "news": "news_score", "miner_score": "miner_fused", "fastformer": "ff_fused",
+           "corpus": "rk_fused"}[family]
     if t.get("workload") != workload or t.get("batch") != B:
         PMC_STATUS[key] = f"rejected: measured {t.get('workload')} x {t.get('batch')}, not {workload} x {B}"
     elif t.get("source_sha16") != want:
@@ -545,7 +546,8 @@ def run_news(args, rank, world, dev):
     # the dense-row comparison line first: measured after the minute of fp32 / bf16 news launches
     # below it read 3.53-3.59 ms, in isolation every version of the kernel since round-1 v8 reads
     # 3.26-3.37 ms (tools/bisect_dense.py, profiles/r02_dense_bisect.txt)
-    dense = dense_kernel_line(dev) if (world == 1 and not args.no_dense) else None
+    dense = dense_kernel_line(dev, pmc_paths={"bf16": args.traffic, "fp32": args.traffic_dense32}) \
+        if (world == 1 and not args.no_dense) else None
 
     # headline: fp32 (the reference's precision) on the fp16 matrix cores (exact-sum fp16 pairs)
     el32, pre32, kern32, o32, nt32 = measure_news(table32, W1, Q, W2, pool, args.steps, args.warmup, world, dev,
@@ -578,10 +580,14 @@ def run_news(args, rank, world, dev):
 
         ms_l = _kernel_ms(loss_fn, 3, 1, dev)
         assert torch.isfinite(res[0][1]).all()
-        loss_line = {"kernel": "news_score_x2<weighted, dense, 12 chunks, LOSS> (scores + per-impression "
-                               "disagreement D, loss.py:81)", "value": round(B * C / (ms_l / 1e3), 1),
+        pmcl = load_pmc(args.news_traffic32_loss, f"news_L{L}_K{K}_d{D}_C{C}_N{N_NEWS}_fp32_loss", B, "news_x2")
+        loss_line = {"kernel": "news_score_x2<weighted, dense, 12 chunks, MIND shape, LOSS> (scores + per-impression "
+                               "disagreement D, loss.py:81; the Gram spread over the four mui waves)",
+                     "value": round(B * C / (ms_l / 1e3), 1),
                      "unit": "pairs/s", "ms_per_launch": round(ms_l, 4), "impressions": B,
-                     "vs_plain_kernel": round(kern32 / ms_l, 4)}
+                     "vs_plain_kernel": round(kern32 / ms_l, 4),
+                     "traffic": pmcl.get("hbm_bytes_per_launch") if pmcl else None,
+                     "mfma_busy_pmc": pmcl.get("mfma_busy_frac") if pmcl else None}
         del res
     # every history full (hist_len = L, no left padding): the masked-slot grouping saves nothing here
     full_hist = None
@@ -617,8 +623,8 @@ def run_news(args, rank, world, dev):
                 "ms_per_step": round(elw / n_w * 1e3, 4), "kernel_ms_rank0": round(kernw, 4)}
         del pw_
     c2 = config2_line(args, rank, world, dev) if not args.no_config2 else None
-    c4 = config4_subline(dev) if (world == 1 and not args.no_config2) else None
-    c5 = config5_subline(dev) if (world == 1 and not args.no_config2) else None
+    c4 = config4_subline(dev, pmc_path=args.traffic_ff) if (world == 1 and not args.no_config2) else None
+    c5 = config5_subline(dev, pmc_path=args.traffic_rk) if (world == 1 and not args.no_config2) else None
     wide = wide_news_subline(dev) if (world == 1 and not args.no_config2) else None
 
     if rank != 0:
@@ -682,7 +688,7 @@ def run_news(args, rank, world, dev):
     print(json.dumps(line), flush=True)
 
 
-def dense_kernel_line(dev, B=32768, steps=10):
+def dense_kernel_line(dev, B=32768, steps=10, pmc_paths=None):
     """The fused dense-row kernel (the drop-in Miner.score module path, model.py:61-138: weights per
     impression, miner_score) on the config-3 shape, bf16 and fp32 (the reference's precision), each
     with its roofline (FLOPs 2LdDc + 2LDcK + 2KLd + 2Kd² + 4CdK + 2CK per impression: MFMA-bound)."""
@@ -717,11 +723,19 @@ def dense_kernel_line(dev, B=32768, steps=10):
         del imp
         kname = {"bf16": "miner_fused<bf16,full>", "fp32": "miner_fused<fp32,full,bf16x6 S1/S5>",
                  "fp32_mfma_exact": "miner_fused<fp32,full>"}[name]
+        # the counter files of the two default forms (tools/r06_pmc.sh), bound to miner_score.hip's sha
+        pmc = None
+        if pmc_paths and name in pmc_paths:
+            pmc = load_pmc(pmc_paths[name], f"L{L}_K{K}_d{D}_Dc{DC}_C{C}_{'bf16' if name == 'bf16' else 'fp32'}",
+                           n, "miner_score")
         out[name] = {"kernel": kname, "value": round(n * C / (ms / 1e3), 1), "unit": "pairs/s",
                      "ms_per_launch": round(ms, 4), "impressions": n,
                      "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
                                   "frac": round(tf / peak, 4), "flops_per_launch": fl,
-                                  "hbm_frac": round(by / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}}
+                                  "hbm_frac": round(by / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+                                  "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                                  "traffic_over_algorithmic": round(pmc["hbm_bytes_per_launch"] / by, 4) if pmc else None,
+                                  "mfma_busy_pmc": pmc.get("mfma_busy_frac") if pmc else None}}
     if prev is None:
         os.environ.pop("MINER_DENSE_FP32", None)
     else:
@@ -916,7 +930,7 @@ def _kernel_ms(fn, steps, warmup, dev):
     return a.elapsed_time(b) / steps
 
 
-def config4_subline(dev, steps=5, warmup=2):
+def config4_subline(dev, steps=5, warmup=2, pmc_path=None):
     """BASELINE config 4 (FastFormer, 50k impressions, bf16) measured inside the default run, so the
     driver's bench carries it; the full line is ``--workload fastformer``."""
     from miner_amd import fastformer as ff
@@ -935,11 +949,16 @@ def config4_subline(dev, steps=5, warmup=2):
     ms = _kernel_ms(fn, steps, warmup, dev)
     assert torch.isfinite(out[0]).all()
     tflops = ff_flops_per_impression() * FF_B / (ms / 1e3) / 1e12
+    pmc = load_pmc(pmc_path, f"ff_L{FF_L}_H{FF_H}_C{FF_C}_bf16_dense", FF_B, "fastformer") if pmc_path else None
     return {"workload": "config 4 FastFormer user encoder (L=50, hidden 256, 16 heads, 2 layers, C=40)",
             "value": round(FF_B * FF_C / (ms / 1e3), 1), "unit": "pairs/s", "dtype": "bf16",
             "impressions_per_step": FF_B, "ms_per_step": round(ms, 4), "steps": steps,
             "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "kernel": "ff_fused<bf16>"}}
+                         "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "kernel": "ff_fused<bf16>",
+                         "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                         "mfma_busy_pmc": pmc.get("mfma_busy_frac") if pmc else None,
+                         "valu_insts_per_impression": round(pmc["SQ_INSTS_VALU"] / FF_B, 1)
+                         if pmc and "SQ_INSTS_VALU" in pmc else None}}
 
 
 WN_B, WN_L, WN_K = 100_000, 100, 64      # the wide news-id line: K = 64, L = 100
@@ -1001,7 +1020,7 @@ def wide_news_subline(dev, steps=5, warmup=2):
                                    "max_abs_diff_x_rms": d_old}}
 
 
-def config5_subline(dev, steps=2, warmup=1, share_users=C5_SHARE_U):
+def config5_subline(dev, steps=2, warmup=1, share_users=C5_SHARE_U, pmc_path=None):
     """BASELINE config 5 (full-corpus ranking: 2048 users x 200k news, L=200, K=64, fp16, top-100) measured
     inside the default run; the full line is ``--workload corpus``."""
     from miner_amd import corpus, synthetic
@@ -1021,6 +1040,8 @@ def config5_subline(dev, steps=2, warmup=1, share_users=C5_SHARE_U):
 
     ms = _kernel_ms(fn, steps, warmup, dev)
     assert torch.isfinite(out[0][0]).all()
+    rk_pmc = load_pmc(pmc_path, f"rk_U{C5_U}_N{C5_N}_L{C5_L}_K{C5_K}_d{D}_top{C5_TOPK}_fp16", C5_U, "corpus") \
+        if pmc_path else None
     fl = C5_U * C5_N * 4 * C5_K * D
     tflops = fl / (ms / 1e3) / 1e12
     # one GPU's share of config 5's 1M users on 8 GPUs (125,000), ranked in one host loop
@@ -1051,7 +1072,9 @@ def config5_subline(dev, steps=2, warmup=1, share_users=C5_SHARE_U):
             "ms_per_step": round(ms, 3), "steps": steps,
             "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tflops / PEAK_BF16_TFLOPS, 4),
-                         "kernel": "ue_fused<fp16> + rk_fused<fp16> (ranker FLOPs over the whole step)"},
+                         "kernel": "ue_fused<fp16> + rk_fused<fp16> (ranker FLOPs over the whole step)",
+                         "ranker_traffic": rk_pmc.get("hbm_bytes_per_launch") if rk_pmc else None,
+                         "ranker_mfma_busy_pmc": rk_pmc.get("mfma_busy_frac") if rk_pmc else None},
             "per_gpu_share": share}
 
 
@@ -1238,6 +1261,10 @@ def main():
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 / -4 / -5 sub-lines")
     ap.add_argument("--no-metrics", action="store_true", help="skip the device metric step")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--traffic-dense32", default=os.path.join(ROOT, "profiles", "pmc_traffic_dense_fp32.json"))
+    ap.add_argument("--traffic-ff", default=os.path.join(ROOT, "profiles", "pmc_traffic_ff_bf16.json"))
+    ap.add_argument("--traffic-rk", default=os.path.join(ROOT, "profiles", "pmc_traffic_rk_fp16.json"))
+    ap.add_argument("--news-traffic32-loss", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_x2_loss.json"))
     ap.add_argument("--news-traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_news.json"))
     ap.add_argument("--news-traffic32", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_x2.json"))
     ap.add_argument("--news-traffic32x", default=os.path.join(ROOT, "profiles", "pmc_traffic_news_fp32.json"))

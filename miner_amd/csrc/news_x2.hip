@@ -66,6 +66,8 @@ namespace {
 #define X2_ABL 0
 #endif
 
+// (1024 / 2048: the mui / X waves skip the history softmax after the first impression, keeping the
+// last A)
 // (eval-loss form, GS: 64 no diagonal Gram tile, 128 no operand exchange / off-diagonal tile, 256 no
 // per-chunk Gram work, 512 no per-impression D step)
 constexpr int kNB = 2;                                // row-DMA blocks per wave per part
@@ -1012,7 +1014,9 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
           if (cp == 0) {
             using std::integral_constant;
             // <= 32 history groups: the softmax over the first 32 only (the second block's A unused)
-            if (nkb == 1) softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 8>{});
+            if ((X2_ABL & 1024) && P == 0 && ci > 0) {                 // timing only: the mui waves keep the last A
+            } else if ((X2_ABL & 2048) && P == 1 && ci > 0) {          // timing only: the X waves keep the last A
+            } else if (nkb == 1) softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 8>{});
             else softmax_inwave(ci, kt, P, aH, aL, kap, integral_constant<int, 16>{});
             if (LOSS && !GS && gram_w && dis_out) {
               float kap1;                // interest tile 1 of the Gram: the Gram's cosines are per-k scale free

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--B", type=int, default=50000)
     ap.add_argument("--L", type=int, default=50)
     ap.add_argument("--C", type=int, default=40)
+    ap.add_argument("--dense", action="store_true", help="dense [B, L, H] rows (bench.py config4_subline), not ids")
     a = ap.parse_args()
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.dtype]
     dev = "cuda:0"
@@ -31,6 +32,13 @@ def main():
     offs = beh.cand_offsets
     run = lambda: ff.score_gather(table, beh.his_ids, beh.his_mask, beh.cand_ids, packed, cand_offsets=offs,
                                   validate=False)
+    if a.dense:                    # the bench's config-4 sub-line inputs (bench.py config4_subline)
+        g = torch.Generator().manual_seed(1000)
+        lens = torch.randint(0, a.L + 1, (a.B,), generator=g)
+        mask = (torch.arange(a.L)[None, :] >= (a.L - lens)[:, None]).to(dev)
+        hist = (torch.randn(a.B, a.L, 256, generator=g) * 0.0625).to(dev, dt)
+        cand = (torch.randn(a.B, a.C, 256, generator=g) * 0.0625).to(dev, dt)
+        run = lambda: ff.score(hist, mask, cand, packed)
     for _ in range(2):
         run()
     torch.cuda.synchronize()

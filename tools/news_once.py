@@ -1,8 +1,9 @@
 """Run the news-path scoring kernel `reps` times at config-3 shape (for rocprofv3 passes).
 
-    python tools/news_once.py [fp32|bf16] [B] [reps] [d] [n_news] [full]
+    python tools/news_once.py [fp32|bf16] [B] [reps] [d] [n_news] [full|pad] [loss]
 
-``full``: every history holds L clicks (the bench's full_histories sub-line).
+``full``: every history holds L clicks (the bench's full_histories sub-line); ``loss``: the
+eval-loss form (the per-impression disagreement D formed in the kernel, the bench's eval_with_loss).
 
 fp32 runs the fp16-pair kernel news_score_x2 unless MINER_NEWS_FP32=mfma32 (news_score32). d = 256
 with n_news = 65238 is config 2.
@@ -32,7 +33,9 @@ hid[~mask] = 0
 cid = torch.randint(1, n_news, (B, C), generator=g, device=dev, dtype=torch.int32)
 W1, Q, W2 = synthetic.init_weights(36, d, Dc, K, device=dev)
 nt = news.precompute(table, ops.pack_weights(W1, Q, W2, dtype=dt))
+loss = len(sys.argv) > 7 and sys.argv[7] == "loss"
 for _ in range(reps):
-    s = news.score(nt, hid, mask, cid, validate=False)
+    s = news.score(nt, hid, mask, cid, validate=False, disagreement=loss)
+    s = s[0] if loss else s
 torch.cuda.synchronize()
 print("ok", float(s.float().abs().mean()))

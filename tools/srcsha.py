@@ -13,6 +13,7 @@ KERNEL_SOURCES = {
     "news": ("miner_amd/csrc/news.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_news.h"),
     "miner_score": ("miner_amd/csrc/miner_score.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_score.h"),
     "fastformer": ("miner_amd/csrc/fastformer.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_fastformer.h"),
+    "corpus": ("miner_amd/csrc/corpus.hip", "miner_amd/csrc/cdna4_common.h", "include/miner_corpus.h"),
 }
 
 
