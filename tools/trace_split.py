@@ -1,5 +1,5 @@
 """Per-launch durations of the headline kernel from a rocprofv3 kernel trace, split by bench phase:
-the bench launches news_score_x2<0, false, 12, 2, false, false> first for its main line (W warmup + K timed
+the bench launches news_score_x2<0, false, 12, 2, false> first for its main line (W warmup + K timed
 steps), later again for the full-history sub-line, so the trace's overall average mixes the two.
 
     python tools/trace_split.py TRACE_CSV [--warmup 5] [--steps 20] > summary.json
@@ -9,7 +9,7 @@ import csv
 import json
 import statistics
 
-HEADLINE = "news_score_x2<0, false, 12, 2, false, false>"   # <ST, RAGGED, NCH, SHP, LOSS, R3>
+HEADLINE = "news_score_x2<0, false, 12, 2, false>"   # <ST, RAGGED, NCH, SHP, LOSS>
 
 ap = argparse.ArgumentParser()
 ap.add_argument("trace")
