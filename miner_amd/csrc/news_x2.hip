@@ -851,9 +851,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // the next chunk's row DMAs, issued by every wave right after the barrier. (Round 6 A/B,
   // tools/x2_ab.py, 1M impressions: the mui waves — which set the chunk length — issuing theirs
   // after their history product instead +3.1 %; the mui waves at priority 2 while they issue
-  // +2.2 %; profiles/r06_x2_dma_ab.txt; the X waves — 450-550 cycles of barrier slack per chunk —
-  // issuing theirs after their history product, so the mui waves' DMAs meet fewer at the barrier:
-  // +1.5 %, profiles/r06_x2_dma_late_x_ab.txt)
+  // +2.2 %; profiles/r06_x2_dma_ab.txt)
   int dn_cc = 0, dn_ni = 0, dn_np = 0;
   auto issue_dmas = [&]() {
     if (dn_cc + 1 < nchunk) {
