@@ -179,6 +179,17 @@ __device__ __forceinline__ f32x4 mfma_x2(f32x4 c, const u32x4& ah, const u32x4& 
   c = mfma_h(ah, bl, c);
   return mfma_h(ah, bh, c);
 }
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16_h(unsigned a0, unsigned a1, unsigned b0, unsigned b1, f32x4 c) {
+  typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4, u32x2v{a0, a1}),
+                                                __builtin_bit_cast(f16x4, u32x2v{b0, b1}), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16_x2(f32x4 c, const u32x4& a, const u32x4& b) {
+  c = mfma16_h(a[2], a[3], b[0], b[1], c);
+  c = mfma16_h(a[0], a[1], b[2], b[3], c);
+  return mfma16_h(a[0], a[1], b[0], b[1], c);
+}
 // two fp32 values -> (hi, lo) fp16 pairs, packed. The residual is taken against the hi bits as
 // packed: left to itself hipcc packs hi with v_cvt_pk_f16_f32 but recomputes the f32 value of hi
 // with a separate v_cvt_f16_f32, and the two round some halfway cases differently (one fp16 ulp of
@@ -373,12 +384,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   const bool path_live = P == 0 || WEIGHTED;
   // The eval loss's Gram. GS (the MIND shape: L = 50, 4 or 12 chunks): spread over the four mui
   // waves — each adds its own diagonal 16x16 tile over its 32 columns from the operand of its
-  // candidate product (no extra split); the off-diagonal tile goes to the interest-tile-0 waves,
-  // which get the tile-1 operand of the same columns through LDS one chunk later (rows 56..63 of
-  // part ch of that chunk's ring slot: no DMA writes them at L <= 52, and the history product reads
-  // them times an attention weight of exactly 0, so only their finiteness matters). Otherwise (run-
-  // time shapes) waves 0 and 2 run the history product for both interest tiles and add all three
-  // tiles of their 32 columns.
+  // candidate product (no extra split); the off-diagonal tile is split by column tile: the wave of
+  // interest tile kt adds G_{kt,1-kt} over columns [16 kt, +16) of its column half, with the other
+  // wave's operand of those columns through LDS one chunk later (rows 56..63 of part ch of that
+  // chunk's ring slot: no DMA writes them at L <= 52, and the history products read zero rows in
+  // their place, trH3). Otherwise (run-time shapes) waves 0 and 2 run the history product for both
+  // interest tiles and add all three tiles of their 32 columns.
   constexpr bool GS = LOSS && SHP == 2;
   static_assert(!GS || (NCH >= 3 && WEIGHTED), "the spread Gram: chunk counts >= 3, 'weighted' scoring");
   const bool gram_w = LOSS && P == 0 && (GS || kt == 0);
@@ -569,7 +580,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   // group receives column i of the 4 rows: contraction index 8g + e <-> row 32 kb + 16 (e >> 2) + 4g +
   // (e & 3), the order of the Ā tiles (softmax_inwave). Candidate reads: row i (+ 16 ct rows = 4096 B),
   // columns 32 ch + 16 ctl + 4g .. + 3 (8 B).
-  uint32_t trH[2][2], trL[2][2], cfH[2], cfL[2];
+  // GS: the second block's rows 56..63 hold the Gram exchange (any bits, NaN included), so the
+  // lanes that would read them (groups 2, 3 of read rr = 1) read rows 52..55 instead: zeros (no DMA
+  // writes rows >= 52 at L <= 52), times the same zero attention weights (trH3 / trL3)
+  uint32_t trH[2][2], trL[2][2], cfH[2], cfL[2], trH3[2], trL3[2];
   {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, i = lane & 15;
@@ -581,6 +595,12 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         const int chunk = 4 * ch + 2 * ctl + (pp >> 1);
         trH[ctl][rr] = row * kRB + ((chunk ^ x2swz(row)) << 4) + 8 * (pp & 1);
         trL[ctl][rr] = row * kRB + (((chunk + 8) ^ x2swz(row)) << 4) + 8 * (pp & 1);
+      }
+      {
+        const int row = g >= 2 ? 52 + q : 48 + 4 * g + q;
+        const int chunk = 4 * ch + 2 * ctl + (pp >> 1);
+        trH3[ctl] = row * kRB + ((chunk ^ x2swz(row)) << 4) + 8 * (pp & 1);
+        trL3[ctl] = row * kRB + (((chunk + 8) ^ x2swz(row)) << 4) + 8 * (pp & 1);
       }
       const int chunk = 4 * ch + 2 * ctl + (g >> 1);
       cfH[ctl] = i * kRB + ((chunk ^ x2swz(i)) << 4) + 8 * (g & 1);
@@ -674,7 +694,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
 #pragma unroll
   for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   int pend_d = -1;                               // impression whose D is formed at the next chunk (wave 0)
-  u32x4 gpH = u32x4{0u, 0u, 0u, 0u}, gpL = gpH;   // GS, tile-0 waves: this wave's operand of the last chunk
+  u32x4 gp = u32x4{0u, 0u, 0u, 0u};   // GS: this wave's operand of its off-diagonal columns, the last chunk
   int gs_step = 0, gs_b = 0;                     // GS (kernel-uniform): D of impression gs_b, step 1 / 2 pending
   int nkb = 2;                                   // 32-row blocks of unique history rows of the item
   bool d_pending = false;                        // wave-uniform: a Gram hand-off is waiting
@@ -714,68 +734,63 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
     for (int q = 0; q < 3; ++q) gr[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
-  // GS. The exchange block of chunk tt's tile-1 operand of column half ch: [hi 64 lanes x 16 B | lo]
-  auto gs_xbuf = [&](int tt) { return smem + (tt & 1) * Cv::kSlot + ch * Cv::kPart + 56 * kRB; };
-  // the tile-1 operand of the chunk before (tile-0 waves), read right after each chunk's barrier
-  // and used at the end of its products (the off-diagonal tile (0, 1) with this wave's own operand
-  // of that chunk, gpH / gpL) or by the D step: its LDS latency hides behind the chunk's work
-  u32x4 gxH = u32x4{0u, 0u, 0u, 0u}, gxL = gxH;
+  // GS. The exchange block written by the wave of interest tile w in chunk tt, column half ch: 64
+  // lanes x 16 B {hi, hi | lo, lo} of the columns the other wave takes, [16 (1 - w), +16)
+  auto gs_xbuf = [&](int tt, int w) { return smem + (tt & 1) * Cv::kSlot + ch * Cv::kPart + 56 * kRB + w * 1024; };
+  // the other wave's operand of this wave's off-diagonal columns in the chunk before, read right
+  // after each chunk's barrier and used at the end of its products (with this wave's own operand
+  // of those columns in that chunk, gp) or by the D step: its LDS latency hides behind the chunk
+  u32x4 gx = u32x4{0u, 0u, 0u, 0u};
   auto gs_read = [&]() {
     if (X2_ABL & (128 | 256)) return;
-    const char* xb = gs_xbuf(t - 1) + 16 * (threadIdx.x & 63);
-    gxH = *reinterpret_cast<const u32x4*>(xb);
-    gxL = *reinterpret_cast<const u32x4*>(xb + 1024);
+    gx = *reinterpret_cast<const u32x4*>(gs_xbuf(t - 1, 1 - kt) + 16 * (threadIdx.x & 63));
   };
+  // rows = this wave's own interests: the tile-1 wave's partial is the (0, 1) tile transposed, so
+  // the D step weighs it with the norms the other way round
   auto gs_offdiag = [&]() {
     if (X2_ABL & (128 | 256)) return;
-    gr[1] = mfma_x2(gr[1], gpH, gpL, gxH, gxL);
+    gr[1] = mfma16_x2(gr[1], gp, gx);
   };
-  // per chunk of a Gram pass, after the operand split (mui waves): the diagonal tile; the tile-0
-  // waves take the previous chunk's off-diagonal tile and keep their operand for the next; the
-  // tile-1 waves publish theirs — a non-finite one as zeros: the block is read by the history
-  // products times 0, and the wave's own diagonal tile already carries it into the norms, so D
-  // stays NaN / inf as the reference's. (Round 6 A/B, tools/x2_ab.py: the same code on every mui
-  // wave — the tile-1 waves' off-diagonal products on zeros, to avoid moving register tuples
-  // between branches — measured +2.6 %.)
-  auto gs_chunk = [&](int cc, const float* x, const u32x4& bH, const u32x4& bL) {
+  // per chunk of a Gram pass, after the operand split (mui waves): the diagonal tile; the previous
+  // chunk's off-diagonal partial; this wave's operand of its off-diagonal columns kept for the
+  // next, the other columns' published as they are (a non-finite operand too: only this pass's
+  // off-diagonal products read the block, and the wave's own diagonal tile carries it into the
+  // norms anyway, so D is NaN / inf as the reference's). Round 6 A/B (tools/x2_ab.py):
+  // the whole off-diagonal tile on the tile-0 waves +0.4 %; the published operand checked for
+  // finiteness and zeroed, while the history products still read these rows, +3.2 %.
+  auto gs_chunk = [&](int cc, const u32x4& bH, const u32x4& bL) {
     if (X2_ABL & 256) return;
     if (!(X2_ABL & 64)) gr[0] = mfma_x2(gr[0], bH, bL, bH, bL);
     if (X2_ABL & 128) return;
-    if (kt == 0) {
-      if (cc > 0) gs_offdiag();
-      gpH = bH;
-      gpL = bL;
-    } else {
-      // |x| < 2^14 when finite, so the sum of the 8 is finite exactly when all 8 are
-      const float sx = ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
-      const bool fin = __builtin_isfinite(sx);
-      char* xb = gs_xbuf(t) + 16 * (threadIdx.x & 63);
-      *reinterpret_cast<u32x4*>(xb) = fin ? bH : u32x4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(xb + 1024) = fin ? bL : u32x4{0u, 0u, 0u, 0u};
-    }
+    if (cc > 0) gs_offdiag();
+    const u32x4 c0 = u32x4{bH[0], bH[1], bL[0], bL[1]}, c1 = u32x4{bH[2], bH[3], bL[2], bL[3]};
+    gp = kt ? c1 : c0;
+    *reinterpret_cast<u32x4*>(gs_xbuf(t, kt) + 16 * (threadIdx.x & 63)) = kt ? c0 : c1;
   };
-  // step 1 (the chunk after a Gram pass, after its barrier; mui waves): the last off-diagonal tile,
-  // the norms n_k = sqrt(G_kk) from the four waves' diagonal partials (LDS [ch][kt][16], written at
-  // the pass end), this wave's share Σ G_kk' / (n_k n_k') over its tiles (k != k', (0, 1) twice) ->
-  // LDS; step 2 (a chunk later, wave 0): D = (Σ of the four shares) / K²
+  // step 1 (the chunk after a Gram pass, after its barrier; mui waves): the last off-diagonal
+  // partial, the norms n_k = sqrt(G_kk) from the four waves' diagonal partials (LDS [ch][kt][16],
+  // written at the pass end), this wave's share Σ G_kk' / (n_k n_k') over its tiles (k != k' in the
+  // diagonal tile, the off-diagonal partial twice) -> LDS; step 2 (a chunk later, wave 0): D = (Σ
+  // of the four shares) / K²
   auto gs_step1 = [&]() {
     if (P != 0 || (X2_ABL & 512)) return;
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, g = lane >> 4;
-    if (kt == 0) gs_offdiag();
+    gs_offdiag();
     // 1 / n_k = rsq(G_kk) (rsq(inf) = 0 and rsq(0) = inf keep a non-finite or zero mui NaN in D,
-    // as the reference's cosines); lane (g, j) needs rows m = 4g..4g+3 of its tile and column j
+    // as the reference's cosines); lane (g, j) needs rows m = 4g..4g+3 of its tile, column j of its
+    // tile (diagonal) and of the other (off-diagonal)
     const float* gdg = reinterpret_cast<const float*>(smem + Cv::kOffGram);
     const f32x4 dm0 = *reinterpret_cast<const f32x4*>(gdg + kt * 16 + 4 * g);
     const f32x4 dm1 = *reinterpret_cast<const f32x4*>(gdg + 32 + kt * 16 + 4 * g);
     const float rj = __builtin_amdgcn_rsqf(gdg[kt * 16 + j] + gdg[32 + kt * 16 + j]);
-    const float rj1 = __builtin_amdgcn_rsqf(gdg[16 + j] + gdg[48 + j]);
+    const float rj1 = __builtin_amdgcn_rsqf(gdg[(1 - kt) * 16 + j] + gdg[32 + (1 - kt) * 16 + j]);
     float sum = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float rm = __builtin_amdgcn_rsqf(dm0[e] + dm1[e]);
       if (4 * g + e != j) sum = __builtin_fmaf(gr[0][e] * rm, rj, sum);
-      if (kt == 0) sum = __builtin_fmaf(2.0f * gr[1][e] * rm, rj1, sum);
+      sum = __builtin_fmaf(2.0f * gr[1][e] * rm, rj1, sum);
     }
     // over the 16 lanes of a row (DPP row rotations), then the 4 rows (permlane swaps)
     sum += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sum), 0x128, 0xf, 0xf, false));
@@ -875,8 +890,10 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       u32x4 eH[2], eL[2];
 #pragma unroll
       for (int ctl = 0; ctl < 2; ++ctl) {
-        const uint2 h0 = lds_tr(part + trH[ctl][0] + 8192 * kb), h1 = lds_tr(part + trH[ctl][1] + 8192 * kb);
-        const uint2 l0 = lds_tr(part + trL[ctl][0] + 8192 * kb), l1 = lds_tr(part + trL[ctl][1] + 8192 * kb);
+        const uint2 h0 = lds_tr(part + trH[ctl][0] + 8192 * kb);
+        const uint2 h1 = lds_tr(part + ((GS && kb) ? trH3[ctl] : trH[ctl][1] + 8192 * kb));
+        const uint2 l0 = lds_tr(part + trL[ctl][0] + 8192 * kb);
+        const uint2 l1 = lds_tr(part + ((GS && kb) ? trL3[ctl] : trL[ctl][1] + 8192 * kb));
         eH[ctl] = u32x4{h0.x, h0.y, h1.x, h1.y};
         eL[ctl] = u32x4{l0.x, l0.y, l1.x, l1.y};
       }
@@ -948,7 +965,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
       }
       u32x4 bH, bL;
       split8h(x, bH, bL);
-      if (GS && (mode & 8)) gs_chunk(cc, x, bH, bL);
+      if (GS && (mode & 8)) gs_chunk(cc, bH, bL);
       X2_STAMP(5);
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
@@ -998,7 +1015,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
         // the unit merge waits (compiler vmcnt) for the loads of the previous dedupe: here, before
         // this chunk's DMAs are issued, they have landed and the wait is free
         if ((!LOSS || SHP == 2) && cp == 0 && cc == 0) dedupe_merge();
-        if (GS && gram_w && kt == 0 && (need_g || gs_step == 1)) gs_read();
+        if (GS && gram_w && (need_g || gs_step == 1)) gs_read();
         // the next chunk's row DMAs right after the barrier, before a pass start's S7 / softmax / aux
         // work (round 4: -0.9 %)
         dn_cc = cc; dn_ni = ni; dn_np = np;
@@ -1119,7 +1136,7 @@ __global__ __launch_bounds__(kThreads) void news_score_x2(X2Params p) {
   if (WITH_CAND && pend_off >= 0) s7();
   if (LOSS && pend_d >= 0) form_d(pend_d);
   if (GS && gs_step == 1) {
-    if (gram_w && kt == 0) gs_read();
+    if (gram_w) gs_read();
     gs_step1();
     raw_barrier();
     gs_step2();
