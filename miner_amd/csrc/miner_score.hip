@@ -204,10 +204,76 @@ __device__ unsigned long long g_stage_imps;
 #ifndef MINER_X6_STAGES
 #define MINER_X6_STAGES 5   // bf16x6 stages of the fp32 kernel: 1 S1, 2 S4, 4 S5, 8 S6 (S4 spills 12-21 VGPRs, S6 61-74: off)
 #endif
+#ifndef MINER_S1_P2
+#define MINER_S1_P2 1   // fp32 (bf16x6 form, cooperative S1 cut): S1 on fp16 pairs (0: bf16x6, A/B builds)
+#endif
+#ifndef MINER_S5_P2
+#define MINER_S5_P2 1   // fp32 (bf16x6 form): S5 on fp16 pairs (0: bf16x6, A/B builds)
+#endif
 template <class T, bool X6>
 __device__ __forceinline__ void mma_f(f32x16& acc, const Frag<T>& a, const Frag<T>& b) {
   if constexpr (X6 && sizeof(T) == 4) mma_slab_x6(acc, a, b);
   else mma_slab<T>(acc, a, b);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp16 pairs (the fp32 kernel's S5, news_x2.hip's operand form): an fp32 value x of a row with unit
+// u (a power of two, max|row| < 2^14·u) is carried as hi = f16(x/u), lo = f16(x/u - hi), and a
+// product as lo·hi + hi·lo + hi·hi on the f16 MFMA: three v_mfma_f32_32x32x16_f16 per 16-element
+// step instead of bf16x6's six, the weights pre-cut at pack time (same bytes as fp32: no split VALU
+// for them). The accumulator is rescaled by the two rows' units (powers of two: exact).
+// ---------------------------------------------------------------------------------------------
+// row unit exponent: max|row| < 2^e (a non-finite max is clamped to FLT_MAX: e = 128)
+__host__ __device__ inline int p2_exp(float mx) {
+  int e;
+  frexpf(mx, &e);
+  return e < -100 ? -100 : (e > 128 ? 128 : e);
+}
+// 2^(e - 14) and 2^(14 - e), the unit and the splitting scale of a row with max|row| < 2^e
+__host__ __device__ inline float p2_unit(int e) { return ldexpf(1.0f, e - 14); }
+__host__ __device__ inline float p2_scale(int e) { return ldexpf(1.0f, 14 - e); }
+// the unit of a row with max|row| = mx: +inf when the row holds an infinity (its finite elements
+// scale to 0 and the infinity is clamped, p2_split2), so its products come out ±inf — or NaN for a
+// zero weight — as the reference's w·inf
+__host__ __device__ inline float p2_unit_of(float mx, int e) { return mx > 3.40282347e38f ? INFINITY : p2_unit(e); }
+// (x0, x1), scaled so that a finite row's |x| < 2^14, -> packed (hi, lo) fp16 pairs; the residual
+// against hi as packed (one conversion of hi). An infinite x is clamped to ±65504 (v_med3: a NaN
+// passes through), hi = ±65504 and lo = 0, so no inf - inf; its row's unit is +inf (p2_unit_of).
+template <bool CLAMP = true>   // false: the caller has clamped
+__device__ __forceinline__ void p2_split2(float x0, float x1, unsigned& hi, unsigned& lo) {
+  if constexpr (CLAMP) {
+    x0 = __builtin_amdgcn_fmed3f(x0, -65504.0f, 65504.0f);
+    x1 = __builtin_amdgcn_fmed3f(x1, -65504.0f, 65504.0f);
+  }
+  const f16x2v h = __builtin_convertvector((f32x2v){x0, x1}, f16x2v);
+  unsigned hb = __builtin_bit_cast(unsigned, h);
+  asm volatile("" : "+v"(hb));
+  const f16x2v hh = __builtin_bit_cast(f16x2v, hb);
+  hi = hb;
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){x0 - (float)hh[0], x1 - (float)hh[1]}, f16x2v));
+}
+__device__ __forceinline__ f32x16 mfma32_f16(const u32x4& a, const u32x4& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// acc += A·B over one 32-wide slab: A a pair-packed weight fragment (pieces {hi, lo} of elements
+// 0..7, then of 8..15), B an fp32 fragment already scaled and clamped, cut here (smallest products
+// first)
+__device__ __forceinline__ void mma_slab_p2(f32x16& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    u32x4 bh, bl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = 8 * st + 2 * i;
+      unsigned h, l;
+      p2_split2<false>(__uint_as_float(b.q[e >> 2][e & 3]), __uint_as_float(b.q[(e + 1) >> 2][(e + 1) & 3]), h, l);
+      bh[i] = h;
+      bl[i] = l;
+    }
+    acc = mfma32_f16(a.q[2 * st + 1], bh, acc);
+    acc = mfma32_f16(a.q[2 * st], bl, acc);
+    acc = mfma32_f16(a.q[2 * st], bh, acc);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -216,9 +282,12 @@ __device__ __forceinline__ void mma_f(f32x16& acc, const Frag<T>& a, const Frag<
 // X_m = gelu(W2[tile m] · muiᵀ) over the whole contraction d; packed W2 slabs stream from L2
 // through a PF-deep register ring (unconditional loads, clamped at the end), muiᵀ fragments come
 // from LDS.  The result stays in registers as slab fragments of the S6 contraction.
-template <class T, int PF, int NM, bool X6>
+// P2 (fp32): W2p is the pair-packed copy, u2 its row units, s2 + 32 the units of the 32 mui rows
+// (muiL scaled in place by their inverses, infinities clamped)
+template <class T, int PF, int NM, bool X6, bool P2 = false>
 __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restrict__ W2p, const T* muiL,
-                                        int msE, int d, int wave, int lane) {
+                                        int msE, int d, int wave, int lane, const float* __restrict__ u2 = nullptr,
+                                        const float* s2 = nullptr) {
   const int ns = d >> 5;
   const int r = lane & 31, h = lane >> 5;
   f32x16 acc[NM];
@@ -241,7 +310,10 @@ __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restric
       Frag<T> bm;
       frag_load(bm, muiL + r * msE + (j + s) * 32 + 16 * h);
 #pragma unroll
-      for (int m = 0; m < NM; ++m) mma_f<T, X6 && (MINER_X6_STAGES & 4)>(acc[m], ring[s][m], bm);
+      for (int m = 0; m < NM; ++m) {
+        if constexpr (P2) mma_slab_p2(acc[m], ring[s][m], bm);
+        else mma_f<T, X6 && (MINER_X6_STAGES & 4)>(acc[m], ring[s][m], bm);
+      }
 #pragma unroll
       for (int m = 0; m < NM; ++m) frag_load_tile(ring[s][m], w2t[m] + min(j + s + PF, ns - 1) * 1024, lane);
       __builtin_amdgcn_sched_barrier(0);   // keep the refill right behind the MFMAs it waits on
@@ -253,7 +325,20 @@ __device__ __forceinline__ void s5_gelu(Frag<T> (&xf)[kMaxJ], const T* __restric
       Frag<T> bm;
       frag_load(bm, muiL + r * msE + (j + s) * 32 + 16 * h);
 #pragma unroll
-      for (int m = 0; m < NM; ++m) mma_f<T, X6 && (MINER_X6_STAGES & 4)>(acc[m], ring[s][m], bm);
+      for (int m = 0; m < NM; ++m) {
+        if constexpr (P2) mma_slab_p2(acc[m], ring[s][m], bm);
+        else mma_f<T, X6 && (MINER_X6_STAGES & 4)>(acc[m], ring[s][m], bm);
+      }
+    }
+  }
+  if constexpr (P2) {
+    // the units back: register e of lane half h is W2 row 32 tile + 16h + e, column r is mui row r
+    const float ub = s2[32 + r];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const float* ur = u2 + (wave + kWaves * m) * 32 + 16 * h;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][e] = acc[m][e] * ur[e] * ub;
     }
   }
 #pragma unroll
@@ -456,6 +541,14 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
   const T* __restrict__ W1p = static_cast<const T*>(p.wp);
   const T* __restrict__ Qp = W1p + w1p_elems(d, Dc);
   const T* __restrict__ W2p = Qp + qp_elems(Dc);
+  // fp32 (bf16x6 form): S5 on fp16 pairs — the pair-packed W2 copy and its row units follow W2p
+  constexpr bool kP2 = !kBf16 && X6 && MODE == kFull && MINER_S5_P2;
+  const T* __restrict__ W2x = W2p + w2p_elems(d);
+  const float* __restrict__ u2 = reinterpret_cast<const float*>(W2x + w2p_elems(d));
+  // ... and S1 (the cooperative cut form) likewise: the pair-packed W1 copy and its row units
+  constexpr bool kP1 = kS1Coop && MINER_S1_P2;
+  const T* __restrict__ W1x = reinterpret_cast<const T*>(u2 + d);
+  const float* __restrict__ u1 = reinterpret_cast<const float*>(W1x + w1p_elems(d, Dc));
   const bool weighted = (p.score_type == MINER_SCORE_WEIGHTED);
   const bool need_scores = (p.score_type != MINER_SCORE_NONE);
   const int rowB = d * 2;
@@ -530,9 +623,30 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         f32x16 cacc0 = zero16(), cacc1 = zero16();
         constexpr bool coop = kS1Coop;
         if constexpr (coop) {
+          // kP1: each history row's splitting scale and unit ([64 scales | 64 units] in the S region,
+          // free until S2) from one pass over the rows (8 lanes per row)
+          [[maybe_unused]] float* s1L = reinterpret_cast<float*>(smem + p.offS);
+          if constexpr (kP1) {
+            const int row = tid >> 3, c = tid & 7;
+            const T* er = erow(min(row, L - 1));
+            float mx = 0.f;
+            for (int i = 4 * c; i < d; i += 32) {
+              const float4 v = *reinterpret_cast<const float4*>(er + i);
+              mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 1));
+            mx = fmaxf(mx, __shfl_xor(mx, 2));
+            mx = fmaxf(mx, __shfl_xor(mx, 4));
+            if (c == 0) {
+              const int e = p2_exp(fminf(mx, 3.40282347e38f));
+              s1L[row] = p2_scale(e);
+              s1L[64 + row] = p2_unit_of(mx, e);
+            }
+            __syncthreads();
+          }
           // rounds of two slabs through two LDS buffers: round g + 1 is cut (its global loads in
           // flight) while round g's products run, one barrier per round
-          const T* w1t = W1p + (size_t)min(wave, nct - 1) * ns * 1024;
+          const T* w1t = (kP1 ? W1x : W1p) + (size_t)min(wave, nct - 1) * ns * 1024;
           Frag<T> ring1;
           frag_load_tile(ring1, w1t, lane);
           auto cut = [&](int g) {          // slabs g, g + 1 -> buffer (g / 2) & 1
@@ -542,19 +656,33 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
               const float4* src = reinterpret_cast<const float4*>(erow(min(row, L - 1)) + (g + sl) * 32 + c8);
               const float4 x0 = src[0], x1 = src[1];
               const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-              u32x4 hi, md, lo;
-#pragma unroll
-              for (int m = 0; m < 4; ++m) {
-                unsigned a, b, c;
-                split3_pair<true>(xv[2 * m], xv[2 * m + 1], a, b, c);
-                hi[m] = a;
-                md[m] = b;
-                lo[m] = c;
-              }
               char* dst = sb + sl * kS1Slab + row * kS1Row + c8 * 2;
-              *reinterpret_cast<u32x4*>(dst) = hi;
-              *reinterpret_cast<u32x4*>(dst + kS1Plane) = md;
-              *reinterpret_cast<u32x4*>(dst + 2 * kS1Plane) = lo;
+              if constexpr (kP1) {       // fp16 pairs: planes hi | lo
+                const float sc = s1L[row];
+                u32x4 hi, lo;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                  unsigned a, b;
+                  p2_split2(xv[2 * m] * sc, xv[2 * m + 1] * sc, a, b);
+                  hi[m] = a;
+                  lo[m] = b;
+                }
+                *reinterpret_cast<u32x4*>(dst) = hi;
+                *reinterpret_cast<u32x4*>(dst + kS1Plane) = lo;
+              } else {
+                u32x4 hi, md, lo;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                  unsigned a, b, c;
+                  split3_pair<true>(xv[2 * m], xv[2 * m + 1], a, b, c);
+                  hi[m] = a;
+                  md[m] = b;
+                  lo[m] = c;
+                }
+                *reinterpret_cast<u32x4*>(dst) = hi;
+                *reinterpret_cast<u32x4*>(dst + kS1Plane) = md;
+                *reinterpret_cast<u32x4*>(dst + 2 * kS1Plane) = lo;
+              }
             }
           };
           cut(0);
@@ -571,15 +699,28 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
                   const char* base = sb + s2 * kS1Slab;
 #pragma unroll
                   for (int st = 0; st < 2; ++st) {
-                    u32x4 ah, am, al;
-                    split8_step<false>(a, st, ah, am, al);
+                    if constexpr (kP1) {   // a: pair pieces {hi, lo} of step st; lo·hi + hi·lo + hi·hi
 #pragma unroll
-                    for (int rt = 0; rt < 2; ++rt) {
-                      const char* q = base + (32 * rt + r) * kS1Row + (16 * h + 8 * st) * 2;
-                      const u32x4 bh = *reinterpret_cast<const u32x4*>(q);
-                      const u32x4 bm = *reinterpret_cast<const u32x4*>(q + kS1Plane);
-                      const u32x4 bl = *reinterpret_cast<const u32x4*>(q + 2 * kS1Plane);
-                      mma6_step(rt ? cacc1 : cacc0, ah, am, al, bh, bm, bl);
+                      for (int rt = 0; rt < 2; ++rt) {
+                        const char* q = base + (32 * rt + r) * kS1Row + (16 * h + 8 * st) * 2;
+                        const u32x4 bh = *reinterpret_cast<const u32x4*>(q);
+                        const u32x4 bl = *reinterpret_cast<const u32x4*>(q + kS1Plane);
+                        f32x16& c = rt ? cacc1 : cacc0;
+                        c = mfma32_f16(a.q[2 * st + 1], bh, c);
+                        c = mfma32_f16(a.q[2 * st], bl, c);
+                        c = mfma32_f16(a.q[2 * st], bh, c);
+                      }
+                    } else {
+                      u32x4 ah, am, al;
+                      split8_step<false>(a, st, ah, am, al);
+#pragma unroll
+                      for (int rt = 0; rt < 2; ++rt) {
+                        const char* q = base + (32 * rt + r) * kS1Row + (16 * h + 8 * st) * 2;
+                        const u32x4 bh = *reinterpret_cast<const u32x4*>(q);
+                        const u32x4 bm = *reinterpret_cast<const u32x4*>(q + kS1Plane);
+                        const u32x4 bl = *reinterpret_cast<const u32x4*>(q + 2 * kS1Plane);
+                        mma6_step(rt ? cacc1 : cacc0, ah, am, al, bh, bm, bl);
+                      }
                     }
                   }
                 }
@@ -666,6 +807,21 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
             }
           }
           STAMP(10);
+          if constexpr (kP1) {
+            // the units back: register e of lane half h is W1 row 32 wave + 16h + e, column r (+ 32)
+            // history row r (32 + r)
+            const float* s1L = reinterpret_cast<const float*>(smem + p.offS);
+            const float v0 = s1L[64 + r], v1 = s1L[96 + r];
+            const float* ur = u1 + wave * 32 + 16 * h;
+            // (the padded rows c >= Dc stay 0, also beside a history row of unit +inf: Q is zero
+            // there, and 0·NaN would poison S)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const bool cv = 32 * wave + 16 * h + e < Dc;
+              acc0[e] = cv ? acc0[e] * ur[e] * v0 : 0.f;
+              acc1[e] = cv ? acc1[e] * ur[e] * v1 : 0.f;
+            }
+          }
 #pragma unroll
           for (int e = 0; e < 16; ++e) { acc0[e] = act_tanh<T>(acc0[e]); acc1[e] = act_tanh<T>(acc1[e]); }
           STAMP(11);
@@ -918,13 +1074,40 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
     if (need_scores) {
       // ---- S5: X = gelu(W2 · muiᵀ), wave-owned d-tiles kept in registers ---------------------
       Frag<T> xf[kMaxJ];
+      // kP2: each mui row's unit (s2L[32 + k], in the dead Aw region); mui scaled in place by its inverse
+      float* s2L = reinterpret_cast<float*>(smem + p.offAw);
+      if constexpr (kP2) {
+        if (weighted) {
+          FRESH_LANE_IDS();
+          const int k = tid >> 4, c = tid & 15;     // 16 lanes (a DPP row) per mui row
+          float mx = 0.f;
+          for (int i = 4 * c; i < d; i += 64) {
+            const float4 v = *reinterpret_cast<const float4*>(muiL + k * msE + i);
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          }
+          mx = row16_max(mx);
+          const int e = p2_exp(fminf(mx, 3.40282347e38f));
+          if (c == 0) s2L[32 + k] = p2_unit_of(mx, e);
+          // the row scaled in place (a power of two: exact) and an infinity clamped (p2_split2), once
+          // here instead of in each wave's S5 split; S6 takes the units back from its products
+          const float sc = p2_scale(e);
+          for (int i = 4 * c; i < d; i += 64) {
+            float4* q = reinterpret_cast<float4*>(muiL + k * msE + i);
+            const float4 v = *q;
+            *q = float4{__builtin_amdgcn_fmed3f(v.x * sc, -65504.0f, 65504.0f), __builtin_amdgcn_fmed3f(v.y * sc, -65504.0f, 65504.0f),
+                        __builtin_amdgcn_fmed3f(v.z * sc, -65504.0f, 65504.0f), __builtin_amdgcn_fmed3f(v.w * sc, -65504.0f, 65504.0f)};
+          }
+          __syncthreads();
+        }
+      }
       {
         FRESH_LANE_IDS();
         const int nm = (ns - wave + kWaves - 1) / kWaves;
+        const T* w2s = kP2 ? W2x : W2p;
         if (weighted) {
-          if (nm == 3) s5_gelu<T, PF, 3, X6>(xf, W2p, muiL, msE, d, wave, lane);
-          else if (nm == 2) s5_gelu<T, PF, 2, X6>(xf, W2p, muiL, msE, d, wave, lane);
-          else if (nm == 1) s5_gelu<T, PF, 1, X6>(xf, W2p, muiL, msE, d, wave, lane);
+          if (nm == 3) s5_gelu<T, PF, 3, X6, kP2>(xf, w2s, muiL, msE, d, wave, lane, u2, s2L);
+          else if (nm == 2) s5_gelu<T, PF, 2, X6, kP2>(xf, w2s, muiL, msE, d, wave, lane, u2, s2L);
+          else if (nm == 1) s5_gelu<T, PF, 1, X6, kP2>(xf, w2s, muiL, msE, d, wave, lane, u2, s2L);
         }
       }
       Frag<T> am[kMaxJ];   // bf16 full: the wave's mui fragments, held across the candidate chunks
@@ -948,6 +1131,17 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           lg[0] = lg[1] = mt[0] = mt[1] = zero16();
           if (weighted) s6_dispatch<T, true, MODE == kFull, X6>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
           else s6_dispatch<T, false, MODE == kFull, X6>(nm, lg, mt, xf, am, cand, cimg, Cb, cc, d, wave, r, h, muiL, msE, cids, p.n_news);
+          if constexpr (kP2) {
+            // mui was scaled in place for S5 (weighted): its rows' units back on M (row k of the tile
+            // in register e of lane half h: acc_row)
+            if (weighted) {
+              const float* un = reinterpret_cast<const float*>(smem + p.offAw) + 32;
+#pragma unroll
+              for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) mt[ct][e] *= un[acc_row(e, h)];
+            }
+          }
           STAMP_SYNC();
           STAMP(6);
           if constexpr (kDma) {
@@ -1063,6 +1257,44 @@ __global__ void pack_weights_kernel(const T* __restrict__ W1, const T* __restric
       block_pos<T>((int)(q & 1023), rr, cc);
       const int jt = (int)(tile / ns), j = (int)(tile % ns);
       v = W2[(size_t)(jt * 32 + pi_row(rr)) * d + j * 32 + cc];
+    }
+    out[i] = v;
+  }
+}
+
+// fp32 W2 as fp16 pairs: row units (one thread per row), then the pair tiles — the fp32 tiles'
+// fragment-major geometry (a 16-byte piece per lane and q), piece 2st + plane of lane l holding
+// plane (hi, lo) of that lane's elements 8st..8st+7: [16 (l >> 5) + 8st, +8) of tile row pi(l & 31)
+// W [rows, d] row-major; units for the padded rows (up to 32 per tile) are 1, their pieces 0
+__global__ void pair_units_kernel(const float* __restrict__ W, int rows, int rows_pad, int cols,
+                                  float* __restrict__ units) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_pad) return;
+  float mx = 0.f;
+  if (i < rows)
+    for (int j = 0; j < cols; ++j) mx = fmaxf(mx, fabsf(W[(size_t)i * cols + j]));
+  units[i] = i < rows ? p2_unit_of(mx, p2_exp(fminf(mx, 3.40282347e38f))) : 1.0f;
+}
+__global__ void pack_pairs_kernel(const float* __restrict__ W, const float* __restrict__ units, int rows, int ntr,
+                                  int d, u32x4* __restrict__ out) {
+  const int ns = d >> 5;
+  const size_t n = (size_t)ntr * ns * 256;          // 16-byte pieces
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t tile = i >> 8;
+    const int q = (int)((i >> 6) & 3), l = (int)(i & 63);
+    const int st = q >> 1, plane = q & 1;
+    const int jt = (int)(tile / ns), j = (int)(tile % ns);
+    const int row = jt * 32 + pi_row(l & 31);
+    const int c0 = j * 32 + 16 * (l >> 5) + 8 * st;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (row < rows) {
+      const float s = 1.0f / units[row];             // a power of two: exact
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        unsigned hi, lo;
+        p2_split2(W[(size_t)row * d + c0 + 2 * m] * s, W[(size_t)row * d + c0 + 2 * m + 1] * s, hi, lo);
+        v[m] = plane ? lo : hi;
+      }
     }
     out[i] = v;
   }
@@ -1224,9 +1456,12 @@ int run(void* stream, int dtype_in, int mode, Params prm) {
   return gather ? launch<float, kFull, 0, true, 0, true>(stream, prm, c.total) : launch<float, kFull, 0, false, 0, true>(stream, prm, c.total);
 }
 
+// fp32: [W1p | Qp | W2p | W2 pair-packed | W2 row units | W1 pair-packed | W1 row units (n_ctiles·32)];
+// bf16: [W1p | Qp | W2p]
 size_t packed_bytes(int dtype, int d, int Dc) {
   const size_t es = dtype == MINER_DTYPE_BF16 ? 2 : 4;
-  return (w1p_elems(d, Dc) + qp_elems(Dc) + w2p_elems(d)) * es;
+  const size_t pairs = dtype == MINER_DTYPE_BF16 ? 0 : w2p_elems(d) + (size_t)d + w1p_elems(d, Dc) + qp_elems(Dc) / 32;
+  return (w1p_elems(d, Dc) + qp_elems(Dc) + w2p_elems(d) + pairs) * es;
 }
 
 }  // namespace
@@ -1252,10 +1487,25 @@ int miner_pack_weights(void* stream, int dtype, const void* w_poly, const void* 
     hipLaunchKernelGGL(pack_weights_kernel<__bf16>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
                        static_cast<const __bf16*>(w_poly), static_cast<const __bf16*>(context_codes),
                        static_cast<const __bf16*>(w_target), d, Dc, K, static_cast<__bf16*>(packed));
-  else
-    hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       static_cast<const float*>(w_poly), static_cast<const float*>(context_codes),
-                       static_cast<const float*>(w_target), d, Dc, K, static_cast<float*>(packed));
+  else {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<const float*>(w_poly),
+                       static_cast<const float*>(context_codes), static_cast<const float*>(w_target), d, Dc, K,
+                       static_cast<float*>(packed));
+    // the fp16-pair copies of W2 (S5) and W1 (S1) with their row units
+    float* w2x = static_cast<float*>(packed) + w1p_elems(d, Dc) + qp_elems(Dc) + w2p_elems(d);
+    float* u2 = w2x + w2p_elems(d);
+    float* w1x = u2 + d;
+    float* u1 = w1x + w1p_elems(d, Dc);
+    auto pairs = [&](const float* W, int rows, int ntr, float* x, float* units) {
+      hipLaunchKernelGGL(pair_units_kernel, dim3((ntr * 32 + 255) / 256), dim3(256), 0, s, W, rows, ntr * 32, d, units);
+      const size_t pieces = (size_t)ntr * (d >> 5) * 256;
+      const int g2 = (int)((pieces + 255) / 256 < 4096 ? (pieces + 255) / 256 : 4096);
+      hipLaunchKernelGGL(pack_pairs_kernel, dim3(g2), dim3(256), 0, s, W, units, rows, ntr, d, reinterpret_cast<u32x4*>(x));
+    };
+    if (w_target) pairs(static_cast<const float*>(w_target), d, d >> 5, w2x, u2);
+    pairs(static_cast<const float*>(w_poly), Dc, n_ctiles(Dc), w1x, u1);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? MINER_OK : (int)e;
 }

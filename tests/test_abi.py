@@ -98,8 +98,11 @@ def test_lds_fits_one_cu(lib):
 
 def test_packed_bytes(lib):
     assert lib.miner_packed_weights_bytes(_lib.DTYPE_BF16, 768, 200, 32) > 2 * (768 * 768 + 200 * 768)
+    # fp32: the bf16 layout's tiles at 4 bytes, then the fp16-pair copies of W2 and W1 (same bytes as
+    # their fp32 tiles) and their row units (d, and Dc padded to 32-row tiles)
+    w1, w2 = 7 * 24 * 1024, 24 * 24 * 1024
     assert lib.miner_packed_weights_bytes(_lib.DTYPE_F32, 768, 200, 32) == \
-        2 * lib.miner_packed_weights_bytes(_lib.DTYPE_BF16, 768, 200, 32)
+        2 * lib.miner_packed_weights_bytes(_lib.DTYPE_BF16, 768, 200, 32) + 4 * (w2 + 768 + w1 + 7 * 32)
     assert lib.miner_packed_weights_bytes(_lib.DTYPE_F32, 100, 200, 32) == 0
 
 

@@ -251,3 +251,74 @@ def test_x6_infinite_history_element(monkeypatch):
     assert orc.parity_ok(mui[fin].numpy(), ref_mui[fin].numpy())[0]
     ok_rows = [b for b in range(B) if b not in (3, 5)]
     assert orc.parity_ok(s.cpu()[ok_rows].numpy(), ref[ok_rows].numpy())[0]
+
+
+@pytest.mark.parametrize("score_type", ["weighted", "max"])
+def test_fp32_pairs_heavy_tailed(score_type, monkeypatch):
+    """The default fp32 form runs S1 (W1·Eᵀ) and S5 (W2·muiᵀ) on fp16 pairs with a power-of-two unit
+    per operand row (history row, mui row, weight row). Heavy-tailed inputs, as encoder outputs have
+    them: three dimensions 100x the rest in every row, history / candidate rows 1e4x and 1e5x the
+    median norm in impressions 0-79 (0-19 / 20-39 in the history, 40-59 / 60-79 as a candidate),
+    and weight rows 30x the rest. Against float64 (oracle.score_f64), on the impressions that touch
+    the outliers and on the others separately (each with its own rms, so an outlier row cannot hide
+    the error of the ordinary ones): within 1.5x the fp32 MFMA's error, and the fp32 bar — except on
+    the outlier impressions under 'weighted', where the softmax over K is one-hot and ill-conditioned
+    in any fp32 arithmetic: there the pair form stays within 1.5x the error of the reference's own
+    fp32 path (the oracle's CPU restatement, ATen ops in model.py's order)."""
+    g = torch.Generator().manual_seed(83)
+    B, L, C, d, Dc, K, n = 160, 50, 40, 768, 200, 32, 3000
+    T = torch.randn((n, d), generator=g) / d ** 0.5
+    T[:, [5, 77, d // 2 + 16]] *= 100.0
+    T[1] *= 1e4
+    T[2] *= 1e5
+    hid = torch.randint(3, n, (B, L), generator=g)
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    mask = torch.arange(L)[None, :] >= (L - lens)[:, None]
+    hid[~mask] = 0
+    cid = torch.randint(3, n, (B, C), generator=g)
+    hid[0:20, L - 1] = 1
+    hid[20:40, L - 1] = 2
+    cid[40:60, 7] = 1
+    cid[60:80, 3] = 2
+    E, cand = T[hid], T[cid]
+    W1 = torch.randn((Dc, d), generator=g) * (2.0 / (Dc + d)) ** 0.5
+    Q = torch.randn((K, Dc), generator=g) * (2.0 / (K + Dc)) ** 0.5
+    W2 = torch.randn((d, d), generator=g) * (1.0 / d) ** 0.5
+    W1[:4] *= 30.0
+    W2[:16] *= 30.0
+    _, ref = orc.score_f64(E.numpy(), mask.numpy(), cand.numpy(), W1.numpy(), Q.numpy(), W2.numpy(), score_type)
+    ref = torch.from_numpy(ref)
+    subsets = {"outlier": slice(0, 80), "ordinary": slice(80, None)}
+    errs = {}
+    for form in ("pairs", "mfma32"):
+        if form == "mfma32":
+            monkeypatch.setenv("MINER_DENSE_FP32", "mfma32")
+        else:
+            monkeypatch.delenv("MINER_DENSE_FP32", raising=False)
+        s = _ops().score(E.to(DEV), mask.to(DEV), cand.to(DEV), W1.to(DEV), Q.to(DEV), W2.to(DEV),
+                         score_type=score_type).double().cpu()
+        torch.cuda.synchronize()
+        for name, sl in subsets.items():
+            r, x = ref[sl], s[sl]
+            rms = float(r.pow(2).mean().sqrt())
+            e = (x - r).abs()
+            errs[(form, name)] = (float((e / (r.abs() + rms)).max()), float(e.pow(2).mean().sqrt() / rms))
+            if score_type == "weighted" and name == "outlier":
+                continue
+            ok, worst = orc.parity_ok(x.numpy(), r.numpy())
+            assert ok, f"{form} {score_type} on the {name} impressions: off by {worst:.2f}x the tolerance"
+    for name in subsets:
+        pe, me = errs[("pairs", name)], errs[("mfma32", name)]
+        assert pe[0] <= 1.5 * me[0] + 1e-7, (name, errs)
+        assert pe[1] <= 1.5 * me[1] + 1e-8, (name, errs)
+    if score_type == "weighted":
+        sl = subsets["outlier"]
+        r = ref[sl]
+        rms = float(r.pow(2).mean().sqrt())
+        x32 = orc.score_torch(E, mask, cand, W1, Q, W2, score_type)[1].double()[sl]
+        e = (x32 - r).abs()
+        re = (float((e / (r.abs() + rms)).max()), float(e.pow(2).mean().sqrt() / rms))
+        print(f"outlier/weighted error (max rel, rms rel): reference fp32 {re}, pairs {errs[('pairs', 'outlier')]}, "
+              f"mfma32 {errs[('mfma32', 'outlier')]}")
+        fe = errs[("pairs", "outlier")]      # (the fp32 MFMA form is looser here: its fma order)
+        assert fe[0] <= 1.5 * re[0] + 1e-7 and fe[1] <= 1.5 * re[1] + 1e-8, (fe, re)
