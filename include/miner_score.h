@@ -24,8 +24,8 @@
  *     (a hipStream_t; NULL = the default stream) and the call returns immediately;
  *   - `dtype` selects the element type of the activation AND weight tensors and the arithmetic:
  *     MINER_DTYPE_F32 = fp32 tensors, fp32-class products (the parity mode: within 1e-5 of the
- *     reference's fp32 path; see each entry point for the form, e.g. bf16x6 on the bf16 matrix
- *     cores for miner_score), MINER_DTYPE_F32_MFMA = the same fp32 tensors with every product on
+ *     reference's fp32 path; see each entry point for the form, e.g. fp16 pairs on the fp16
+ *     matrix cores for miner_score), MINER_DTYPE_F32_MFMA = the same fp32 tensors with every product on
  *     the fp32 MFMA (exact fp32 fma chains), MINER_DTYPE_BF16 = bf16 operands with fp32
  *     accumulation, the throughput mode. Masks are uint8 (0/1, torch.bool storage), offsets int32,
  *     bias/scores/user_out fp32;
@@ -100,11 +100,14 @@ int miner_pack_target_weights(void* stream, int dtype, const void* w_target, int
 
 /*
  * Score B impressions.
- * dtype MINER_DTYPE_F32 (the reference's precision): the W1·Eᵀ and W2·muiᵀ contractions run as
- * bf16x6 on the bf16 matrix cores (each fp32 operand cut exactly into three bf16 terms, the six
- * leading partial products, fp32 accumulation; error vs float64 within 1.5x the fp32 MFMA's), the
- * rest on the fp32 MFMA. dtype MINER_DTYPE_F32_MFMA: every product on the fp32 MFMA (exact fp32
- * fma chains; the Python layer passes it under MINER_DENSE_FP32=mfma32).
+ * dtype MINER_DTYPE_F32 (the reference's precision): the W1·Eᵀ and W2·muiᵀ contractions run on
+ * fp16 pairs (each fp32 operand x of a row with a power-of-two unit u carried as hi = f16(x/u),
+ * lo = f16(x/u - hi); lo·hi + hi·lo + hi·hi on the fp16 matrix cores, fp32 accumulation, the units
+ * applied exactly; error vs float64 within 1.5x the fp32 MFMA's), the rest on the fp32 MFMA. The
+ * fp32 packed buffer carries pair copies of W1 and W2 and their row units for this; where the LDS
+ * carve leaves room for two workgroups per CU (small shapes), W1·Eᵀ stays bf16x6 (three bf16 terms
+ * per operand, six partial products). dtype MINER_DTYPE_F32_MFMA: every product on the fp32 MFMA
+ * (exact fp32 fma chains; the Python layer passes it under MINER_DENSE_FP32=mfma32).
  *   history      [B, L, d]  dtype  clicked-news embeddings, left-padded (reader.py:369)
  *   his_mask     [B, L]     uint8  1 = real click, 0 = pad (entities.py:395)
  *   his_bias     [B, L]     fp32   optional category bias, already averaged over the candidates
