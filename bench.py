@@ -699,7 +699,7 @@ def dense_kernel_line(dev, B=32768, steps=10, pmc_paths=None):
     for name, dt, peak, n in (("bf16", torch.bfloat16, PEAK_BF16_TFLOPS, B), ("fp32", torch.float32, PEAK_F32_TFLOPS,
                                                                                B // 4),
                               ("fp32_mfma_exact", torch.float32, PEAK_F32_TFLOPS, B // 4)):
-        # fp32: S1 / S5 as bf16x6 (the default); fp32_mfma_exact: every product on the fp32 MFMA
+        # fp32: S1 / S5 on fp16 pairs (the default); fp32_mfma_exact: every product on the fp32 MFMA
         if name == "fp32_mfma_exact":
             os.environ["MINER_DENSE_FP32"] = "mfma32"
         elif prev is None:
@@ -721,7 +721,7 @@ def dense_kernel_line(dev, B=32768, steps=10, pmc_paths=None):
         tf = fl / (ms / 1e3) / 1e12
         by = bytes_per_impression(L, D, C, 2 if name == "bf16" else 4) * n
         del imp
-        kname = {"bf16": "miner_fused<bf16,full>", "fp32": "miner_fused<fp32,full,bf16x6 S1/S5>",
+        kname = {"bf16": "miner_fused<bf16,full>", "fp32": "miner_fused<fp32,full,fp16-pair S1/S5>",
                  "fp32_mfma_exact": "miner_fused<fp32,full>"}[name]
         # the counter files of the two default forms (tools/r06_pmc.sh), bound to miner_score.hip's sha
         pmc = None
@@ -742,11 +742,13 @@ def dense_kernel_line(dev, B=32768, steps=10, pmc_paths=None):
         os.environ["MINER_DENSE_FP32"] = prev
     out["note"] = ("Miner.score / Miner.forward's drop-in module path on dense [B, L, d] / [B, C, d] rows: every "
                    "impression re-reads W1 and W2 (the news-id path precomputes them per news row instead). fp32: "
-                   "S1 (W1·Eᵀ) and S5 (W2·muiᵀ) as bf16x6 (each fp32 operand cut exactly into three bf16 terms, the "
-                   "six leading partial products on the bf16 MFMA; error vs float64 within 1.5x the fp32 MFMA's, "
-                   "tests/test_gpu_parity.py::test_x6_error_vs_fp32_mfma), S2 / S4 / S6 on the fp32 MFMA; its "
-                   "frac is algorithmic FLOPs over the fp32 peak. fp32_mfma_exact: every product on the fp32 MFMA "
-                   "(MINER_DENSE_FP32=mfma32)")
+                   "S1 (W1·Eᵀ) and S5 (W2·muiᵀ) on fp16 pairs (each fp32 operand of a row with a power-of-two unit u "
+                   "carried as hi = f16(x/u), lo = f16(x/u - hi), lo·hi + hi·lo + hi·hi on the fp16 MFMA, the units "
+                   "applied exactly; W1 / W2 pair copies packed once; error vs float64 within 1.5x the fp32 MFMA's, "
+                   "tests/test_gpu_parity.py::test_x6_error_vs_fp32_mfma, ::test_fp32_pairs_heavy_tailed), S2 / S4 / "
+                   "S6 on the fp32 MFMA; its frac is algorithmic FLOPs over the fp32 peak; traffic counts the history "
+                   "rows three times per impression (the pairs' row-unit pass, S1's cut, S4's gathers: beyond what an "
+                   "XCD's L2 holds for 32 CUs). fp32_mfma_exact: every product on the fp32 MFMA (MINER_DENSE_FP32=mfma32)")
     return out
 
 
