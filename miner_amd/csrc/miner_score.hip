@@ -859,7 +859,27 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
       STAMP(1);
 
       // ---- S2 (fp32; fused into S1 for bf16): Sᵀ[k][l] = Σ_c Q[k][c] P[l][c] ------------------
-      if constexpr (!kBf16) {
+      if constexpr (!kBf16 && kS1Coop) {
+        // the contraction over the context tiles split over all 8 waves (history tile wave & 1, tile
+        // group wave >> 1: tiles cg, cg + 4): four partials [4][K][kMaxL] from offS on (the S region
+        // and the S1 planes behind it, both free here; P ends where they start), summed in S3 —
+        // two waves over all nct tiles left six idle: 12.6k cycles per impression
+        FRESH_LANE_IDS();
+        const int lt = wave & 1, cg = wave >> 1;
+        if (lt * 32 < L) {
+          f32x16 acc = zero16();
+          const T* qrow = Qp + r * (nct * 32) + 16 * h;
+          const T* prow = Ps + (lt * 32 + r) * p.PS + 16 * h;
+          for (int j = cg; j < nct; j += 4) {
+            Frag<T> qa, pb;
+            frag_load(qa, qrow + j * 32);
+            frag_load(pb, prow + j * 32);
+            mma_slab<T>(acc, qa, pb);
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) S[(cg * kMaxK + acc_row(e, h)) * kMaxL + lt * 32 + r] = acc[e];
+        }
+      } else if constexpr (!kBf16) {
         FRESH_LANE_IDS();
         if (wave * 32 < L) {
           f32x16 acc = zero16();
@@ -923,7 +943,10 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
 #pragma unroll
         for (int q = 0; q < RK; ++q) {
           const int k = wave + kWaves * q;
-          v[q] = in ? (real ? S[k * kMaxL + l] + bl : 1e-30f) : -INFINITY;   // model.py:180
+          float sv = S[k * kMaxL + l];
+          if constexpr (kS1Coop)      // the four partials of the split S2
+            sv = ((sv + S[(kMaxK + k) * kMaxL + l]) + S[(2 * kMaxK + k) * kMaxL + l]) + S[(3 * kMaxK + k) * kMaxL + l];
+          v[q] = in ? (real ? sv + bl : 1e-30f) : -INFINITY;   // model.py:180
           m[q] = v[q];
         }
 #pragma unroll
