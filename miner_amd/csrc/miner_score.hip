@@ -621,29 +621,13 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
         // 80-byte rows) instead of by each of the 7 MFMA waves in registers; products and their
         // order per accumulator unchanged (bit-identical)
         f32x16 cacc0 = zero16(), cacc1 = zero16();
+        [[maybe_unused]] int ep0 = 0, ep1 = 0;   // kP1: the accumulators' unit exponents (history rows r, 32 + r)
         constexpr bool coop = kS1Coop;
         if constexpr (coop) {
-          // kP1: each history row's splitting scale and unit ([64 scales | 64 units] in the S region,
-          // free until S2) from one pass over the rows (8 lanes per row)
-          [[maybe_unused]] float* s1L = reinterpret_cast<float*>(smem + p.offS);
-          if constexpr (kP1) {
-            const int row = tid >> 3, c = tid & 7;
-            const T* er = erow(min(row, L - 1));
-            float mx = 0.f;
-            for (int i = 4 * c; i < d; i += 32) {
-              const float4 v = *reinterpret_cast<const float4*>(er + i);
-              mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-            }
-            mx = fmaxf(mx, __shfl_xor(mx, 1));
-            mx = fmaxf(mx, __shfl_xor(mx, 2));
-            mx = fmaxf(mx, __shfl_xor(mx, 4));
-            if (c == 0) {
-              const int e = p2_exp(fminf(mx, 3.40282347e38f));
-              s1L[row] = p2_scale(e);
-              s1L[64 + row] = p2_unit_of(mx, e);
-            }
-            __syncthreads();
-          }
+          // kP1: each history row's unit exponent per round of two slabs (max|row piece| < 2^e, from
+          // the 8 lanes that cut it), [2 buffers][64] ints in the S region (free until S2); the MFMA
+          // waves carry their accumulators from round to round by the exponent difference (exact)
+          [[maybe_unused]] int* reL = reinterpret_cast<int*>(smem + p.offS);
           // rounds of two slabs through two LDS buffers: round g + 1 is cut (its global loads in
           // flight) while round g's products run, one barrier per round
           const T* w1t = (kP1 ? W1x : W1p) + (size_t)min(wave, nct - 1) * ns * 1024;
@@ -652,13 +636,27 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           auto cut = [&](int g) {          // slabs g, g + 1 -> buffer (g / 2) & 1
             char* sb = smem + p.offS1 + ((g >> 1) & 1) * (2 * kS1Slab);
             const int row = tid >> 3, cb = tid & 7, sl = cb >> 2, c8 = (cb & 3) * 8;
+            float4 x0 = float4{0.f, 0.f, 0.f, 0.f}, x1 = x0;
             if (g + sl < ns) {
               const float4* src = reinterpret_cast<const float4*>(erow(min(row, L - 1)) + (g + sl) * 32 + c8);
-              const float4 x0 = src[0], x1 = src[1];
+              x0 = src[0];
+              x1 = src[1];
+            }
+            [[maybe_unused]] float sc = 1.f;
+            if constexpr (kP1) {         // the round's unit of the row: max over its 8 lanes
+              float mx = fmaxf(fmaxf(fmaxf(fabsf(x0.x), fabsf(x0.y)), fmaxf(fabsf(x0.z), fabsf(x0.w))),
+                               fmaxf(fmaxf(fabsf(x1.x), fabsf(x1.y)), fmaxf(fabsf(x1.z), fabsf(x1.w))));
+              mx = fmaxf(mx, __shfl_xor(mx, 1));
+              mx = fmaxf(mx, __shfl_xor(mx, 2));
+              mx = fmaxf(mx, __shfl_xor(mx, 4));
+              const int e = p2_exp(fminf(mx, 3.40282347e38f));
+              if (cb == 0) reL[((g >> 1) & 1) * 64 + row] = e;
+              sc = p2_scale(e);
+            }
+            if (g + sl < ns) {
               const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
               char* dst = sb + sl * kS1Slab + row * kS1Row + c8 * 2;
               if constexpr (kP1) {       // fp16 pairs: planes hi | lo
-                const float sc = s1L[row];
                 u32x4 hi, lo;
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
@@ -691,6 +689,19 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
             if (g + 2 < ns) cut(g + 2);
             if (wave < nct) {
               const char* sb = smem + p.offS1 + ((g >> 1) & 1) * (2 * kS1Slab);
+              if constexpr (kP1) {
+                // this round's exponents; the accumulators (in units 2^(ep - 14)) brought to them
+                const int e0 = reL[((g >> 1) & 1) * 64 + r], e1 = reL[((g >> 1) & 1) * 64 + 32 + r];
+                if (g > 0) {
+#pragma unroll
+                  for (int e = 0; e < 16; ++e) {
+                    cacc0[e] = ldexpf(cacc0[e], ep0 - e0);
+                    cacc1[e] = ldexpf(cacc1[e], ep1 - e1);
+                  }
+                }
+                ep0 = e0;
+                ep1 = e1;
+              }
 #pragma unroll
               for (int s2 = 0; s2 < 2; ++s2) {
                 if (g + s2 < ns) {
@@ -809,9 +820,8 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           STAMP(10);
           if constexpr (kP1) {
             // the units back: register e of lane half h is W1 row 32 wave + 16h + e, column r (+ 32)
-            // history row r (32 + r)
-            const float* s1L = reinterpret_cast<const float*>(smem + p.offS);
-            const float v0 = s1L[64 + r], v1 = s1L[96 + r];
+            // history row r (32 + r), the last round's unit 2^(ep - 14)
+            const float v0 = p2_unit(ep0), v1 = p2_unit(ep1);
             const float* ur = u1 + wave * 32 + 16 * h;
             // (the padded rows c >= Dc stay 0, also beside a history row of unit +inf: Q is zero
             // there, and 0·NaN would poison S)
