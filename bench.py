@@ -747,8 +747,8 @@ def dense_kernel_line(dev, B=32768, steps=10, pmc_paths=None):
                    "applied exactly; W1 / W2 pair copies packed once; error vs float64 within 1.5x the fp32 MFMA's, "
                    "tests/test_gpu_parity.py::test_x6_error_vs_fp32_mfma, ::test_fp32_pairs_heavy_tailed), S2 / S4 / "
                    "S6 on the fp32 MFMA; its frac is algorithmic FLOPs over the fp32 peak; traffic counts the history "
-                   "rows three times per impression (the pairs' row-unit pass, S1's cut, S4's gathers: beyond what an "
-                   "XCD's L2 holds for 32 CUs). fp32_mfma_exact: every product on the fp32 MFMA (MINER_DENSE_FP32=mfma32)")
+                   "rows about twice per impression (S1's cut and S4's gathers: beyond what an XCD's L2 holds for "
+                   "32 CUs). fp32_mfma_exact: every product on the fp32 MFMA (MINER_DENSE_FP32=mfma32)")
     return out
 
 
