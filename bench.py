@@ -736,6 +736,17 @@ def dense_kernel_line(dev, B=32768, steps=10, pmc_paths=None):
                                   "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                                   "traffic_over_algorithmic": round(pmc["hbm_bytes_per_launch"] / by, 4) if pmc else None,
                                   "mfma_busy_pmc": pmc.get("mfma_busy_frac") if pmc else None}}
+        if name == "fp32":
+            # the same run seen on the matrix cores it uses: S1 / S5 (2·L·d·Dc + 2·K·d² per impression)
+            # as three fp16 products each at the fp16 dense peak, S2 / S4 / S6 on the fp32 MFMA
+            f_pair = (2 * L * D * DC + 2 * K * D * D) * n
+            t_s = ms / 1e3
+            out[name]["roofline"]["matrix_cores"] = {
+                "fp16_pair_tflops": round(3 * f_pair / t_s / 1e12, 2), "fp16_peak": PEAK_BF16_TFLOPS,
+                "fp16_frac": round(3 * f_pair / t_s / 1e12 / PEAK_BF16_TFLOPS, 4),
+                "fp32_mfma_tflops": round((fl - f_pair) / t_s / 1e12, 2), "fp32_peak": peak,
+                "note": "frac above = algorithmic fp32 FLOPs over the fp32 peak; the S1 / S5 share runs on the "
+                        "fp16 matrix cores as fp16 pairs (3 products per FLOP), the S2 / S4 / S6 share on the fp32 MFMA"}
     if prev is None:
         os.environ.pop("MINER_DENSE_FP32", None)
     else:
