@@ -26,8 +26,8 @@
  *
  * Conventions are those of miner_score.h (caller-owned 16-byte-aligned device memory, enqueued on
  * `stream`, 0 / negative MINER_E* / positive hipError_t). dtype MINER_DTYPE_F32 is the parity mode
- * (exact fp32 arithmetic), MINER_DTYPE_BF16 the throughput mode (bf16 operands, fp32 accumulation,
- * logits always fp32).
+ * (fp32 tensors, fp32-class products: within 1e-5 of the reference), MINER_DTYPE_BF16 the
+ * throughput mode (bf16 operands, fp32 accumulation, logits always fp32).
  * Limits: L <= 64, K <= 32 with K % 4 == 0, d % 64 == 0 and d <= 1024, Dc <= 256, and at most
  * MINER_NEWS_MAX_CAND candidates per impression (dense C or every ragged C_b).
  */
@@ -51,6 +51,11 @@ extern "C" {
  *   packed_weights              dtype  miner_pack_weights() output (w_target needed for news_proj)
  *   news_logits    [n_news, K]  fp32   out
  *   news_proj      [n_news, d]  dtype  out, or NULL (score_type max / mean need no projection)
+ * dtype MINER_DTYPE_F32: the W1 / W2 products on fp16 pairs (one power-of-two unit per table row
+ * and per weight row, three f16 MFMAs per product: the operand form of the scoring kernels), within
+ * 1.5x the fp32 MFMA's error against float64; MINER_DTYPE_F32_MFMA: every product on the fp32 MFMA
+ * (exact fp32 fma chains; also the form at d = 1024 with Dc = 256, where the pair form's 128 bytes of
+ * row units do not fit beside the 160 KiB carve). Both take the same fp32 packed weights.
  */
 int miner_news_precompute(void* stream, int dtype, const void* news_table, int n_news,
                           const void* packed_weights, int d, int Dc, int K, float* news_logits,

@@ -236,14 +236,19 @@ __host__ __device__ inline float p2_scale(int e) { return ldexpf(1.0f, 14 - e); 
 // scale to 0 and the infinity is clamped, p2_split2), so its products come out ±inf — or NaN for a
 // zero weight — as the reference's w·inf
 __host__ __device__ inline float p2_unit_of(float mx, int e) { return mx > 3.40282347e38f ? INFINITY : p2_unit(e); }
+// an infinity clamped to ±65504 by v_med3, a NaN kept by a select: v_med3 does not return a NaN
+// operand (a NaN table row came out finite in news.hip's pair precompute before the select)
+__device__ __forceinline__ float p2_clamp(float x) {
+  return x != x ? x : __builtin_amdgcn_fmed3f(x, -65504.0f, 65504.0f);
+}
 // (x0, x1), scaled so that a finite row's |x| < 2^14, -> packed (hi, lo) fp16 pairs; the residual
-// against hi as packed (one conversion of hi). An infinite x is clamped to ±65504 (v_med3: a NaN
-// passes through), hi = ±65504 and lo = 0, so no inf - inf; its row's unit is +inf (p2_unit_of).
+// against hi as packed (one conversion of hi). An infinite x is clamped to ±65504 (p2_clamp),
+// hi = ±65504 and lo = 0, so no inf - inf; its row's unit is +inf (p2_unit_of). A NaN stays NaN.
 template <bool CLAMP = true>   // false: the caller has clamped
 __device__ __forceinline__ void p2_split2(float x0, float x1, unsigned& hi, unsigned& lo) {
   if constexpr (CLAMP) {
-    x0 = __builtin_amdgcn_fmed3f(x0, -65504.0f, 65504.0f);
-    x1 = __builtin_amdgcn_fmed3f(x1, -65504.0f, 65504.0f);
+    x0 = p2_clamp(x0);
+    x1 = p2_clamp(x1);
   }
   const f16x2v h = __builtin_convertvector((f32x2v){x0, x1}, f16x2v);
   unsigned hb = __builtin_bit_cast(unsigned, h);
@@ -1127,8 +1132,7 @@ __global__ __launch_bounds__(kThreads) void miner_fused(Params p) {
           for (int i = 4 * c; i < d; i += 64) {
             float4* q = reinterpret_cast<float4*>(muiL + k * msE + i);
             const float4 v = *q;
-            *q = float4{__builtin_amdgcn_fmed3f(v.x * sc, -65504.0f, 65504.0f), __builtin_amdgcn_fmed3f(v.y * sc, -65504.0f, 65504.0f),
-                        __builtin_amdgcn_fmed3f(v.z * sc, -65504.0f, 65504.0f), __builtin_amdgcn_fmed3f(v.w * sc, -65504.0f, 65504.0f)};
+            *q = float4{p2_clamp(v.x * sc), p2_clamp(v.y * sc), p2_clamp(v.z * sc), p2_clamp(v.w * sc)};
           }
           __syncthreads();
         }

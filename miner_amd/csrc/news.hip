@@ -135,15 +135,55 @@ struct PreParams {
   int N, d, Dc, K;
 };
 
+// fp16 pairs for the fp32 precompute (miner_score.hip's operand form, §4 "Round 6"): a row with
+// max|row| < 2^e is carried as x·2^(14-e) = hi + lo, hi = f16, lo = f16(residual), and a product as
+// lo·hi + hi·lo + hi·hi on v_mfma_f32_32x32x16_f16; the accumulator is rescaled by the two rows'
+// units 2^(e-14) (powers of two: exact). The weights' pair copies and units are the ones
+// miner_pack_weights writes for fp32 after W2p: [W2x | u2 (d) | W1x | u1 (32 nct)].
+__device__ __forceinline__ int pre_p2_exp(float mx) {
+  int e;
+  frexpf(mx, &e);
+  return e < -100 ? -100 : (e > 128 ? 128 : e);
+}
+__device__ __forceinline__ f32x16 pre_mfma_f16(const u32x4& a, const u32x4& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// acc += A·B over one 32-wide slab: A a pair-packed weight tile fragment (pieces {hi, lo} of elements
+// 0..7, then of 8..15), B an fp32 fragment already scaled into |x| ≤ 65504, cut here
+__device__ __forceinline__ void pre_slab_p2(f32x16& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    u32x4 bh, bl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = 8 * st + 2 * i;
+      const float x0 = __uint_as_float(b.q[e >> 2][e & 3]), x1 = __uint_as_float(b.q[(e + 1) >> 2][(e + 1) & 3]);
+      const f16x2v hv = __builtin_convertvector((f32x2v){x0, x1}, f16x2v);
+      unsigned hb = __builtin_bit_cast(unsigned, hv);
+      asm volatile("" : "+v"(hb));
+      const f16x2v hh = __builtin_bit_cast(f16x2v, hb);
+      bh[i] = hb;
+      bl[i] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){x0 - (float)hh[0], x1 - (float)hh[1]}, f16x2v));
+    }
+    acc = pre_mfma_f16(a.q[2 * st + 1], bh, acc);
+    acc = pre_mfma_f16(a.q[2 * st], bl, acc);
+    acc = pre_mfma_f16(a.q[2 * st], bh, acc);
+  }
+}
+
 template <class T> constexpr int kPreRows = sizeof(T) == 2 ? 64 : 32;   // news rows per tile
 
 // XOR swizzle of the 16-byte chunks of a tile row (cpr chunks per row, a multiple of 8): the 16
 // rows of a ds_read_b128 lane group land in 16 different bank slots
 __device__ __forceinline__ int pre_swz(int row, int cpr) { return (cpr & 15) ? (row & 7) : (row & 15); }
 
-template <class T, int NS>
+// P2 (fp32 only, MINER_DTYPE_F32): the W1 / W2 products on fp16 pairs (pre_slab_p2) with the
+// pair copies of the packed weights and one unit per table row (the staged rows scaled in place);
+// !P2: every product on the fp32 MFMA (MINER_DTYPE_F32_MFMA)
+template <class T, int NS, bool P2 = false>
 __global__ __launch_bounds__(kThreads) void news_pre(PreParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(!P2 || sizeof(T) == 4, "pairs: fp32 tables");
   constexpr int R = kPreRows<T>;
   constexpr int NRT = R / 32;
   const int d = p.d;
@@ -155,9 +195,14 @@ __global__ __launch_bounds__(kThreads) void news_pre(PreParams p) {
   const int imgB = R * rowB;
   char* img = smem;
   float* xch = reinterpret_cast<float*>(smem + imgB);     // [nct][NRT][16 regs][64 lanes]
+  float* uE = xch + (size_t)nct * NRT * 16 * 64;          // P2: the staged rows' units
   const T* __restrict__ W1p = static_cast<const T*>(p.wp);
   const T* __restrict__ Qp = W1p + w1p_el(d, p.Dc);
   const T* __restrict__ W2p = Qp + qp_el(p.Dc);
+  const T* __restrict__ W2x = W2p + (size_t)(d >> 5) * (d >> 5) * 1024;
+  const float* __restrict__ u2 = reinterpret_cast<const float*>(W2x + (size_t)(d >> 5) * (d >> 5) * 1024);
+  const T* __restrict__ W1x = reinterpret_cast<const T*>(u2 + d);
+  const float* __restrict__ u1 = reinterpret_cast<const float*>(W1x + w1p_el(d, p.Dc));
   const T* __restrict__ tab = static_cast<const T*>(p.table);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = (p.N + R - 1) / R;
@@ -182,11 +227,36 @@ __global__ __launch_bounds__(kThreads) void news_pre(PreParams p) {
     const int n0 = tile * R;
     vm_wait_all();
     raw_barrier();     // the tile's rows landed for every wave; last tile's partial readers done
+    if constexpr (P2) {
+      // each wave scales R / 8 rows in place by 2^(14-e) (an element order inside a row is the
+      // chunk swizzle's: irrelevant to a max and a scale), an infinity clamped to ±65504 by v_med3 and
+      // a NaN kept by a select (v_med3 does not return a NaN operand: a NaN row came out finite,
+      // test_precompute_pairs_heavy_tailed); the row's unit 2^(e-14), +inf for a row holding an infinity
+      const int lane = threadIdx.x & 63;
+#pragma unroll
+      for (int i = 0; i < R / kWaves; ++i) {
+        const int row = (R / kWaves) * wave + i;
+        float* rp = reinterpret_cast<float*>(img + row * rowB);
+        float mx = 0.f;
+        for (int c = lane; c < d; c += 64) mx = fmaxf(mx, fabsf(rp[c]));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        const int e = pre_p2_exp(fminf(mx, 3.40282347e38f));
+        const float sc = ldexpf(1.0f, 14 - e);
+        for (int c = lane; c < d; c += 64) {
+          const float x = rp[c] * sc;
+          rp[c] = x != x ? x : __builtin_amdgcn_fmed3f(x, -65504.0f, 65504.0f);
+        }
+        if (lane == 0) uE[row] = mx > 3.40282347e38f ? INFINITY : ldexpf(1.0f, e - 14);
+      }
+      raw_barrier();
+    }
 
     for (int u = wave; u < J; u += kWaves) {
       FRESH_LANE_IDS();
       const bool w1 = u < nct;
-      const T* blk0 = w1 ? W1p + (size_t)u * ns * 1024 : W2p + (size_t)(u - nct) * ns * 1024;
+      const T* blk0 = P2 ? (w1 ? W1x + (size_t)u * ns * 1024 : W2x + (size_t)(u - nct) * ns * 1024)
+                         : (w1 ? W1p + (size_t)u * ns * 1024 : W2p + (size_t)(u - nct) * ns * 1024);
       f32x16 acc[NRT];
 #pragma unroll
       for (int rt = 0; rt < NRT; ++rt) acc[rt] = zero16();
@@ -199,7 +269,8 @@ __global__ __launch_bounds__(kThreads) void news_pre(PreParams p) {
 #pragma unroll
           for (int q = 0; q < kNQ<T>; ++q)
             ef.q[q] = lds_u32x4(img + row * rowB + (((ch + q) ^ pre_swz(row, cpr)) << 4));
-          mma_slab(acc[rt], wf, ef);
+          if constexpr (P2) pre_slab_p2(acc[rt], wf, ef);
+          else mma_slab(acc[rt], wf, ef);
         }
       };
       if constexpr (NS > 0) {
@@ -220,14 +291,37 @@ __global__ __launch_bounds__(kThreads) void news_pre(PreParams p) {
           step(wf, s);
         }
       }
+      if constexpr (P2) {
+        // register e of lane half h: weight row 32 tile + 16 h + e; column: staged row 32 rt + r
+        const float* uw = (w1 ? u1 + 32 * u : u2 + 32 * (u - nct)) + 16 * h;
+        float wu[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 v = reinterpret_cast<const float4*>(uw)[i];
+          wu[4 * i] = v.x;
+          wu[4 * i + 1] = v.y;
+          wu[4 * i + 2] = v.z;
+          wu[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+          const float ue = uE[32 * rt + r];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[rt][e] = acc[rt][e] * wu[e] * ue;
+        }
+      }
       if (w1) {
         // Sᵀ partial [k, news] = Q[:, tile u] · tanh(Pᵀ)[tile u, news]; Q rows in pi order
         Frag<T> qf;
         frag_load(qf, Qp + (size_t)pi_row(r) * (nct * 32) + 32 * u + 16 * h);
+        // W1's padded rows (c >= Dc) are 0 whatever the table row holds: their zero weights times an
+        // infinite element (or an infinite pair unit) are NaN, and Q's zero columns would carry it
+        // into every logit of the row (the reference has no such rows: tanh(±inf) = ±1)
+        const int cpad = p.Dc - (32 * u + 16 * h);
 #pragma unroll
         for (int rt = 0; rt < NRT; ++rt) {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) acc[rt][e] = nx_tanh<T>(acc[rt][e]);
+          for (int e = 0; e < 16; ++e) acc[rt][e] = e < cpad ? nx_tanh<T>(acc[rt][e]) : 0.f;
           Frag<T> pf;
           acc_to_frag<T>(pf, acc[rt]);
           f32x16 sacc = zero16();
@@ -391,8 +485,13 @@ __global__ __launch_bounds__(kThreads) void news_pre2(PreParams p) {
 #pragma unroll
         for (int jt = 0; jt < 8; ++jt) {
           if (jt < nct) {
+            // padded W1 rows: 0 (news_pre); a NaN kept (tanh_fast's clamp of the exponent drops it)
+            const int cpad = p.Dc - (32 * jt + 16 * h);
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[jt][e] = tanh_fast(acc[jt][e]);
+            for (int e = 0; e < 16; ++e) {
+              const float x = acc[jt][e];
+              acc[jt][e] = e < cpad ? (x != x ? x : tanh_fast(x)) : 0.f;
+            }
             Frag<T> pf, qf;
             acc_to_frag<T>(pf, acc[jt]);
             const char* qa = ql + ((size_t)pi_row(r) * (nct * 32) + 32 * jt + 16 * h) * 2;
@@ -2065,10 +2164,11 @@ int pre_lds(int dtype, int d, int Dc) {
   const int R = dtype == MINER_DTYPE_BF16 ? 64 : 32;
   return R * d * es + n_ct(Dc) * (R / 32) * 16 * 64 * 4;
 }
+constexpr int kPreUnitB = 32 * 4;   // fp32 pairs: the 32 staged rows' units after the partials
 
-template <class T, int NS>
+template <class T, int NS, bool P2 = false>
 int launch_pre(void* stream, const PreParams& prm, int lds) {
-  auto kern = news_pre<T, NS>;
+  auto kern = news_pre<T, NS, P2>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return (int)e;
   const int R = kPreRows<T>;
@@ -2090,18 +2190,19 @@ int launch_pre2(void* stream, const PreParams& prm) {
   return e == hipSuccess ? MINER_OK : (int)e;
 }
 
-template <class T>
+// P2: fp32 on fp16 pairs (MINER_DTYPE_F32); fp32 with P2 false: the fp32 MFMA (MINER_DTYPE_F32_MFMA)
+template <class T, bool P2 = false>
 int run_pre(void* stream, const PreParams& prm, int lds) {
   if constexpr (sizeof(T) == 2) {     // bf16: the GEMM-shaped news_pre2 (round 1 v7: 0.34 -> 0.23 ms)
     return prm.d == 768 ? launch_pre2<24>(stream, prm) : launch_pre2<0>(stream, prm);
   } else {
     switch (prm.d >> 5) {
-      case 2: return launch_pre<T, 2>(stream, prm, lds);
-      case 4: return launch_pre<T, 4>(stream, prm, lds);
-      case 8: return launch_pre<T, 8>(stream, prm, lds);
-      case 16: return launch_pre<T, 16>(stream, prm, lds);
-      case 24: return launch_pre<T, 24>(stream, prm, lds);
-      default: return launch_pre<T, 0>(stream, prm, lds);
+      case 2: return launch_pre<T, 2, P2>(stream, prm, lds);
+      case 4: return launch_pre<T, 4, P2>(stream, prm, lds);
+      case 8: return launch_pre<T, 8, P2>(stream, prm, lds);
+      case 16: return launch_pre<T, 16, P2>(stream, prm, lds);
+      case 24: return launch_pre<T, 24, P2>(stream, prm, lds);
+      default: return launch_pre<T, 0, P2>(stream, prm, lds);
     }
   }
 }
@@ -2212,13 +2313,19 @@ int miner_news_supported(int dtype, int L, int d, int Dc, int K) {
 int miner_news_precompute(void* stream, int dtype, const void* news_table, int n_news, const void* packed_weights,
                           int d, int Dc, int K, float* news_logits, void* news_proj) {
   if (!news_table || !packed_weights || !news_logits || n_news <= 0 || dtype == MINER_DTYPE_F32_X6) return MINER_EINVAL;
+  const bool mfma32 = dtype == MINER_DTYPE_F32_MFMA;   // fp32 tables, every product on the fp32 MFMA
+  if (mfma32) dtype = MINER_DTYPE_F32;
   const int rc = miner_news_supported(dtype, 1, d, Dc, K);
   if (rc != MINER_OK) return rc;
   if (!aligned16(news_table) || !aligned16(packed_weights) || !aligned16(news_logits) || !aligned16(news_proj))
     return MINER_EALIGN;
   PreParams prm{news_table, packed_weights, news_logits, news_proj, n_news, d, Dc, K};
   const int lds = pre_lds(dtype, d, Dc);
-  return dtype == MINER_DTYPE_BF16 ? run_pre<__bf16>(stream, prm, lds) : run_pre<float>(stream, prm, lds);
+  if (dtype == MINER_DTYPE_BF16) return run_pre<__bf16>(stream, prm, lds);
+  // the pair form needs 128 more bytes: at the one shape where the fp32 carve is the whole 160 KiB
+  // (d = 1024, Dc = 256) the fp32-MFMA form runs instead
+  if (mfma32 || lds + kPreUnitB > kLdsMax) return run_pre<float, false>(stream, prm, lds);
+  return run_pre<float, true>(stream, prm, lds + kPreUnitB);
 }
 
 int miner_score_news(void* stream, int dtype, int score_type, const void* news_table, const float* news_logits,

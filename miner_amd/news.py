@@ -160,9 +160,20 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
     else:
         logits = torch.empty((n_news, pw.K), device=table.device, dtype=torch.float32)
         proj = torch.empty((n_news, d), device=table.device, dtype=dtype) if with_proj else None
+    want_x2 = dtype == torch.float32 and (x2_enabled() if x2 is None else x2)
+    if want_x2 and not x2_fits(n_news, d):
+        # the pair-plane kernel addresses a row piece with a 32-bit byte offset (news_x2.hip,
+        # MINER_ESHAPE past it): such a table scores on the fp32-MFMA kernel instead
+        if x2:
+            raise ValueError(f"x2=True: a {n_news} x {d} table is past the pair-plane kernel's 4 GiB "
+                             "row-offset range (n_news * d * 4 < 2^32)")
+        want_x2 = False
+    # fp32: the products on fp16 pairs for the pair-plane kernel (MINER_DTYPE_F32), on the fp32 MFMA
+    # for the fp32-MFMA scoring kernel (MINER_DTYPE_F32_MFMA)
+    pre_dt = _lib.DTYPE_F32_MFMA if dt == _lib.DTYPE_F32 and not want_x2 else dt
     with torch.cuda.device(table.device):
         if not wide_k:
-            rc = _lib.lib().miner_news_precompute(_stream(table.device), dt, _ptr(table), n_news, _ptr(pw.buf), d,
+            rc = _lib.lib().miner_news_precompute(_stream(table.device), pre_dt, _ptr(table), n_news, _ptr(pw.buf), d,
                                                   pw.Dc, pw.K, _ptr(logits), _ptr(proj))
         else:
             from .ops import pack_weights
@@ -172,21 +183,13 @@ def precompute(news_table: Tensor, w_poly, context_codes: Optional[Tensor] = Non
                 first = k0 == 0
                 part = pack_weights(w1, q[k0:k1], w2 if (first and with_proj) else None, dtype=dtype)
                 lg = torch.empty((n_news, k1 - k0), device=table.device, dtype=torch.float32)
-                rc = _lib.lib().miner_news_precompute(_stream(table.device), dt, _ptr(table), n_news, _ptr(part.buf),
+                rc = _lib.lib().miner_news_precompute(_stream(table.device), pre_dt, _ptr(table), n_news, _ptr(part.buf),
                                                       d, pw.Dc, k1 - k0, _ptr(lg), _ptr(proj) if first else None)
                 if rc != 0:
                     break
                 logits[:, k0:k1].copy_(lg)
     _lib.check(rc, "miner_news_precompute")
     planes = None
-    want_x2 = dtype == torch.float32 and (x2_enabled() if x2 is None else x2)
-    if want_x2 and not x2_fits(n_news, d):
-        # the pair-plane kernel addresses a row piece with a 32-bit byte offset (news_x2.hip,
-        # MINER_ESHAPE past it): such a table scores on the fp32-MFMA kernel instead
-        if x2:
-            raise ValueError(f"x2=True: a {n_news} x {d} table is past the pair-plane kernel's 4 GiB "
-                             "row-offset range (n_news * d * 4 < 2^32)")
-        want_x2 = False
     if want_x2:
         o = out.x2 if out is not None and out.x2 is not None else None
         t2, tws = split_x2(table, None if o is None else o.table2, None if o is None else o.table_unit)

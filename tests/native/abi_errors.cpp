@@ -92,6 +92,9 @@ int main() {
   // ---- news path ----
   EXPECT(miner_news_precompute(st, 0, nullptr, 100, buf, 768, 200, 32, fo, buf), 0);
   EXPECT(miner_news_precompute(st, 4, buf, 100, buf, 768, 200, 32, fo, buf), 0);
+  // the fp32-MFMA form goes through the fp32 checks
+  EXPECT(miner_news_precompute(st, MINER_DTYPE_F32_MFMA, buf, 100, buf, 100, 200, 32, fo, buf), MINER_ESHAPE);
+  EXPECT(miner_news_precompute(st, MINER_DTYPE_F32_MFMA, mis, 100, buf, 768, 200, 32, fo, buf), MINER_EALIGN);
   EXPECT(miner_news_precompute(st, 0, buf, -1, buf, 768, 200, 32, fo, buf), 0);
   EXPECT(miner_score_news(st, 0, 0, nullptr, fb, buf, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 32, fo, nullptr), 0);
   EXPECT(miner_score_news(st, 0, 7, buf, fb, buf, 100, ib, ub, nullptr, ib, nullptr, 4, 50, 40, 768, 32, fo, nullptr), 0);

@@ -9,6 +9,8 @@ Tolerances (as tests/test_gpu_parity.py):
   2e-2*rms(ref) (the kernel rounds the attention weights, proj rows and the GELU output to bf16
   MFMA operands).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -281,9 +283,14 @@ def test_x2_heavy_tailed(score_type, monkeypatch):
             assert ke[0] <= 1.5 * re[0] + 1e-7 and ke[1] <= 1.5 * re[1] + 1e-8, (kern, ke, re)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", ["x2", "mfma32", torch.bfloat16])
 @pytest.mark.parametrize("d,Dc,K", [(64, 32, 4), (256, 200, 32), (768, 200, 32), (192, 72, 16)])
-def test_precompute_vs_f64(dtype, d, Dc, K):
+def test_precompute_vs_f64(dtype, d, Dc, K, monkeypatch):
+    """fp32 precompute in both forms (x2: the products on fp16 pairs, MINER_DTYPE_F32; mfma32: on the
+    fp32 MFMA, MINER_DTYPE_F32_MFMA) and bf16, against float64."""
+    if isinstance(dtype, str):
+        monkeypatch.setenv("MINER_NEWS_FP32", dtype)
+        dtype = torch.float32
     g = torch.Generator().manual_seed(d + K)
     n = 333
     table = (torch.randn((n, d), generator=g) / d ** 0.5).to(DEV, dtype)
@@ -299,6 +306,80 @@ def test_precompute_vs_f64(dtype, d, Dc, K):
     else:   # proj is stored in bf16: one rounding of an fp32-accumulated product
         rel = float((nt.proj.double().cpu() - proj).abs().max() / proj.abs().max())
         assert rel < 1e-2, rel
+
+
+def test_precompute_pairs_heavy_tailed():
+    """The pair form of the fp32 precompute carries one power-of-two unit per table row: rows scaled
+    by 2^-60 .. 2^60 keep the fp32 MFMA form's accuracy (within 1.5x its max and rms error against
+    float64, relative to each row's own magnitude), and a row holding an infinity or a NaN gives the
+    reference fp32 arithmetic's pattern of non-finite outputs without touching the other rows of its
+    32-row tile."""
+    d, Dc, K, n = 768, 200, 32, 96
+    g = torch.Generator().manual_seed(606)
+    base = torch.randn((n, d), generator=g) / d ** 0.5
+    scale = torch.pow(2.0, torch.randint(-60, 61, (n, 1), generator=g).double()).float()
+    table = base * scale
+    table[3, 100] = float("inf")
+    table[40, 5] = float("-inf")
+    table[41, 9] = float("nan")
+    W1, Q, W2 = synthetic.init_weights(7, d, Dc, K, device="cpu")
+    W2[11, 100] = 0.0                                  # inf·0 = NaN in the reference's row 3, column 11
+    out = {}
+    for form in ("x2", "mfma32"):
+        os.environ["MINER_NEWS_FP32"] = form
+        try:
+            nt = news.precompute(table.to(DEV), W1.to(DEV), Q.to(DEV), W2.to(DEV))
+            torch.cuda.synchronize()
+            out[form] = (nt.logits.double().cpu(), nt.proj.double().cpu())
+        finally:
+            os.environ.pop("MINER_NEWS_FP32", None)
+    bad = torch.zeros(n, dtype=torch.bool)
+    bad[[3, 40, 41]] = True
+    E = table.double()
+    ref = (torch.tanh(E @ W1.double().T) @ Q.double().T, E @ W2.double().T)
+    ref32 = (torch.tanh(table @ W1.T) @ Q.T, table @ W2.T)
+    for i, name in enumerate(("logits", "proj")):
+        for form in ("x2", "mfma32"):
+            got = out[form][i]
+            # non-finite rows: the reference fp32 pattern (NaN where it is NaN, the same infinities)
+            r32 = ref32[i][bad].double()
+            assert torch.equal(torch.isnan(got[bad]), torch.isnan(r32)), (form, name)
+            fin = torch.isfinite(r32)
+            assert torch.equal(torch.isfinite(got[bad]), fin), (form, name)
+            inf = torch.isinf(r32)
+            assert torch.equal(got[bad][inf], r32[inf]), (form, name)
+        # finite rows: error relative to each row's own magnitude
+        r = ref[i][~bad]
+        rms = r.pow(2).mean(dim=1, keepdim=True).sqrt()
+        errs = {}
+        for form in ("x2", "mfma32"):
+            e = (out[form][i][~bad] - r).abs() / rms
+            errs[form] = (float(e.max()), float(e.pow(2).mean().sqrt()))
+        print(f"{name}: pairs {errs['x2']}, fp32 MFMA {errs['mfma32']}")
+        assert errs["x2"][0] <= 1.5 * errs["mfma32"][0] + 1e-7, (name, errs)
+        assert errs["x2"][1] <= 1.5 * errs["mfma32"][1] + 1e-8, (name, errs)
+
+
+def test_precompute_infinite_row_bf16():
+    """bf16 precompute (news_pre2), Dc = 200 (W1 padded to 224 rows): a table row holding an infinity
+    saturates tanh as in the reference (finite logits), and a NaN row gives NaN logits; the padded
+    rows' zero weights do not turn the infinite row NaN."""
+    d, Dc, K, n = 768, 200, 32, 300
+    g = torch.Generator().manual_seed(607)
+    table = (torch.randn((n, d), generator=g) / d ** 0.5).to(torch.bfloat16)
+    table[3, 100] = float("inf")
+    table[260, 5] = float("-inf")
+    table[261, 9] = float("nan")
+    W1, Q, W2 = [w.to(torch.bfloat16) for w in synthetic.init_weights(8, d, Dc, K, device="cpu")]
+    nt = news.precompute(table.to(DEV), W1.to(DEV), Q.to(DEV), W2.to(DEV))
+    torch.cuda.synchronize()
+    lg = nt.logits.cpu()
+    ref = torch.tanh(table.float() @ W1.float().T) @ Q.float().T
+    assert torch.equal(torch.isnan(lg), torch.isnan(ref))
+    assert torch.isfinite(lg[[3, 260]]).all() and torch.isnan(lg[261]).all()
+    ok = torch.ones(n, dtype=torch.bool)
+    ok[[3, 260, 261]] = False
+    _ok(lg[ok], ref[ok], torch.bfloat16, "logits of the finite rows")
 
 
 # ---- shapes and layouts against the oracle --------------------------------------------------------

@@ -253,6 +253,38 @@ def test_x6_infinite_history_element(monkeypatch):
     assert orc.parity_ok(s.cpu()[ok_rows].numpy(), ref[ok_rows].numpy())[0]
 
 
+@pytest.mark.parametrize("where", ["history", "w_target"])
+def test_pairs_nan_propagates(where, monkeypatch):
+    """A NaN input stays NaN through the fp16-pair operands of the default fp32 form (S1 and S5):
+    the pair clamp keeps it (v_med3 alone would return a finite bound), so the NaN pattern of mui and
+    the scores is the reference's (torch fp32, the reference op order): one impression for a NaN
+    history element, every score for a NaN in W2; everything finite matches at the fp32 bar."""
+    monkeypatch.delenv("MINER_DENSE_FP32", raising=False)
+    g = torch.Generator().manual_seed(72)
+    B, L, C, d, Dc, K = 8, 20, 5, 256, 64, 16
+    E = torch.randn((B, L, d), generator=g) / d ** 0.5
+    cand = torch.randn((B, C, d), generator=g) / d ** 0.5
+    mask = torch.ones((B, L), dtype=torch.bool)
+    W1 = torch.randn((Dc, d), generator=g) * (2.0 / (Dc + d)) ** 0.5
+    Q = torch.randn((K, Dc), generator=g) * (2.0 / (K + Dc)) ** 0.5
+    W2 = torch.randn((d, d), generator=g) * (1.0 / d) ** 0.5
+    if where == "history":
+        E[3, 7, 11] = float("nan")
+    else:
+        W2[40, 9] = float("nan")
+    s, mui = _ops().score(E.to(DEV), mask.to(DEV), cand.to(DEV), W1.to(DEV), Q.to(DEV), W2.to(DEV), return_user=True)
+    torch.cuda.synchronize()
+    ref_mui, ref = orc.score_torch(E, mask, cand, W1, Q, W2)
+    mui, s = mui.cpu(), s.cpu()
+    assert torch.isnan(ref).any()
+    assert torch.equal(torch.isnan(mui), torch.isnan(ref_mui)), "NaN pattern of mui differs from the reference"
+    assert torch.equal(torch.isnan(s), torch.isnan(ref)), "NaN pattern of the scores differs from the reference"
+    fin = torch.isfinite(ref_mui)
+    assert orc.parity_ok(mui[fin].numpy(), ref_mui[fin].numpy())[0]
+    fs = torch.isfinite(ref)
+    assert orc.parity_ok(s[fs].numpy(), ref[fs].numpy())[0]
+
+
 @pytest.mark.parametrize("score_type", ["weighted", "max"])
 def test_fp32_pairs_heavy_tailed(score_type, monkeypatch):
     """The default fp32 form runs S1 (W1·Eᵀ) and S5 (W2·muiᵀ) on fp16 pairs with a power-of-two unit
