@@ -676,9 +676,11 @@ def run_news(args, rank, world, dev):
                            "MFMA with fp32 accumulation; scores within 1e-5 of the reference CPU path "
                            "(auc_parity; tests/test_gpu_news.py: error vs float64 <= the fp32-MFMA kernel's)",
         "roofline": roof,
-        "precompute": {"kernels": "news_pre<fp32> + x2_absmax/x2_split of the table and of proj", "ms": round(pre32, 4),
-                       "flops": pre_fl, "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
-                       "frac_fp32_peak": round(pre_fl / (pre32 / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4)},
+        "precompute": {"kernels": "news_pre<fp32, fp16 pairs> + x2_absmax/x2_split of the table and of proj",
+                       "ms": round(pre32, 4), "flops": pre_fl, "tflops": round(pre_fl / (pre32 / 1e3) / 1e12, 2),
+                       # the W1 / W2 products run as three fp16 MFMAs each (MINER_DTYPE_F32): priced on
+                       # the fp16 dense peak at 3 products per algorithmic FLOP
+                       "frac_fp16_peak_pairs": round(3 * pre_fl / (pre32 / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4)},
         "fp32_mfma_exact": exact, "eval_with_loss": loss_line, "full_histories": full_hist, "weak_scaling": weak,
         "bf16_mode": bf16_mode, "config2": c2, "config4": c4, "config5": c5, "wide_news": wide,
         "metric_step": metric_step,
